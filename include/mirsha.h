@@ -1,0 +1,161 @@
+/*
+ * mirsha.h — C-ABI of the MI355X (gfx950) Actions.Hash engine for MirBFT.
+ *
+ * This is the ONLY native boundary of the drop-in.  Plain pointers and sizes,
+ * no torch / HIP types in the signatures (a hipStream_t is passed as void*).
+ * It replaces the arithmetic of the reference's hash loop
+ *
+ *     for i, req := range actions.Hash {            // processor.go:133
+ *         h := p.Hasher()                           // processor.go:134 (sha256.New)
+ *         for _, data := range req.Data { h.Write(data) }   // :135-137
+ *         actionResults.Digests[i] = &HashResult{Request: req, Digest: h.Sum(nil)} // :139-142
+ *     }
+ *
+ * and the equivalent loops in ProcessorWorkPool (processor.go:312-361, whose
+ * completion-order output is NOT reproduced: every entry point here returns
+ * digests in ORIGIN order) and testengine's Recording (testengine/recorder.go:441-455).
+ * The Go-side binding a maintainer adds is in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Return value: MIRSHA_OK (0) or a negative MIRSHA_E* code; the message is
+ *     available from mirsha_last_error(ctx).  The reference converts processor
+ *     failures into panics (processor.go:75,81,85,91); the Go wrapper does the same.
+ *   - Digests are 32 bytes each, written to digests_out[32*i] for request i.
+ *   - Host-pointer entry points are synchronous: outputs are complete on return.
+ *     Device-pointer entry points (*_device) are asynchronous on the context's
+ *     stream; call mirsha_sync() (or synchronise the stream) before reading.
+ *   - A context is single-caller (not re-entrant), like the reference
+ *     Processor (serialised by its caller, processor.go:447-449).  Each call
+ *     makes the context's device current (cgo may migrate OS threads).
+ */
+#ifndef MIRSHA_H
+#define MIRSHA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIRSHA_OK 0
+#define MIRSHA_EINVAL (-1)   /* bad argument (NULL pointer, range outside arena, ...) */
+#define MIRSHA_EHIP (-2)     /* HIP runtime error */
+#define MIRSHA_ENOMEM (-3)   /* device or pinned allocation failed */
+#define MIRSHA_ERANGE (-4)   /* size limit exceeded (see per-function notes) */
+#define MIRSHA_ENODEV (-5)   /* no usable gfx950 device */
+
+/* Null request marker inside a digest index list: contributes an EMPTY digest
+ * (0 bytes), as a null request's RequestAck.Digest does (client_tracker.go:840-847). */
+#define MIRSHA_NULL_INDEX 0xFFFFFFFFu
+
+/* Largest single message and largest arena one device launch addresses. */
+#define MIRSHA_MAX_MESSAGE_BYTES 0xFFFFFF00u
+#define MIRSHA_MAX_DEVICE_ARENA_BYTES 0xFFFFFF00u
+
+typedef struct mirsha_ctx mirsha_ctx;
+
+int mirsha_version(void); /* (major << 16) | minor */
+
+/* Number of visible devices (hipGetDeviceCount). */
+int mirsha_device_count(int* count);
+
+/* Create / destroy a context bound to one device.  Replaces the per-request
+ * `p.Hasher()` factory (processor.go:21, :58) with one long-lived engine. */
+int mirsha_ctx_create(int device, mirsha_ctx** out);
+void mirsha_ctx_destroy(mirsha_ctx* ctx);
+const char* mirsha_last_error(const mirsha_ctx* ctx);
+
+/* Launch on an external stream (e.g. the caller's current HIP stream) instead
+ * of the context-owned one.  NULL restores the context's own stream. */
+int mirsha_ctx_set_stream(mirsha_ctx* ctx, void* hip_stream);
+void* mirsha_ctx_stream(mirsha_ctx* ctx);
+
+/* Kernel variant for sha256 over packed messages: 0 = LDS-staged coalesced
+ * loader (default), 1 = direct per-lane loads.  For A/B measurement. */
+int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
+
+/* Per-kernel device-time accounting with HIP events on the launch stream.
+ * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator. */
+int mirsha_ctx_set_timing(mirsha_ctx* ctx, int enable);
+int mirsha_ctx_kernel_time(mirsha_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
+int mirsha_ctx_reset_timing(mirsha_ctx* ctx);
+
+/* Wait for all work queued on the context's stream. */
+int mirsha_sync(mirsha_ctx* ctx);
+
+/* ---------------------------------------------------------------- host API */
+
+/* processor.go:129-143 over n requests whose bytes are already concatenated:
+ * request i = arena[off[i] .. off[i]+len[i]).  Any byte alignment.  Lengths
+ * are bucketed by block count internally (longest first); the digest of
+ * request i always lands at digests_out[32*i]. */
+int mirsha_hash_batch(mirsha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
+                      const uint64_t* off, const uint32_t* len, uint32_t n,
+                      uint8_t* digests_out);
+
+/* The same for HashRequest.Data [][]byte (actions.go:157-164) without a
+ * caller-side copy: request i = concat(slice_ptr[s] for s in
+ * [slice_first[i], slice_first[i+1])), slice_first has n+1 entries.
+ * A multi-slice Write sequence hashes exactly its concatenation. */
+int mirsha_hash_slices(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
+                       const uint64_t* slice_len, const uint32_t* slice_first, uint32_t n,
+                       uint8_t* digests_out);
+
+/* Request digests, then the dependent batch digests computed ON DEVICE from
+ * the device-resident request digests (no host round trip):
+ *   batch b = SHA-256(concat(req_digest[idx[e]] for e in [batch_first[b], batch_first[b+1])))
+ * idx[e] == MIRSHA_NULL_INDEX is a null request (0 bytes).  Mirrors
+ * sequence.allocate (sequence.go:154-157) and batchTracker.applyForwardBatchMsg
+ * (batch_tracker.go:147-150) feeding processResults (state_machine.go:394-397). */
+int mirsha_hash_requests_then_batches(mirsha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
+                                      const uint64_t* off, const uint32_t* len, uint32_t n_req,
+                                      const uint32_t* idx, const uint32_t* batch_first,
+                                      uint32_t n_batches, uint8_t* req_digests_out,
+                                      uint8_t* batch_digests_out);
+
+/* Digest lists over caller-provided 32-byte digests (host memory): batch /
+ * VerifyBatch digests over known RequestAck digests, and the testengine
+ * application checkpoint value = Sum of the running hash over the digests
+ * committed since the last reset (testengine/recorder.go:213-256). */
+int mirsha_digest_lists(mirsha_ctx* ctx, const uint8_t* digests, uint32_t n_digests,
+                        const uint32_t* idx, const uint32_t* list_first, uint32_t n_lists,
+                        uint8_t* digests_out);
+
+/* -------------------------------------------------------------- device API */
+/* All pointers are device pointers; asynchronous on the context stream.
+ * arena_len <= MIRSHA_MAX_DEVICE_ARENA_BYTES; reads past arena_len return 0.
+ * order (may be NULL) lists message indices in processing order, e.g. from
+ * mirsha_bucket_order; NULL = identity. */
+int mirsha_hash_batch_device(mirsha_ctx* ctx, const uint8_t* d_arena, uint64_t arena_len,
+                             const uint64_t* d_off, const uint32_t* d_len,
+                             const uint32_t* d_order, uint32_t n, uint8_t* d_digests_out);
+
+int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, const uint32_t* d_idx,
+                               const uint32_t* d_list_first, uint32_t n_lists,
+                               uint8_t* d_digests_out);
+
+/* Host helper: order[] = message indices sorted by SHA-256 block count,
+ * longest first (stable), so a wave's 64 lanes run equal-length chains.
+ * Returns 1 if the order is the identity (all lengths in one bucket), else 0. */
+int mirsha_bucket_order(const uint32_t* len, uint32_t n, uint32_t* order_out);
+
+/* ------------------------------------------------- multi-GPU (one process) */
+/* Shards the n requests by contiguous range across ndev devices (balanced by
+ * block count), one context per device, host gather into origin order.  No
+ * collective: requests are independent (actions.go:22-23). */
+int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena,
+                            uint64_t arena_len, const uint64_t* off, const uint32_t* len,
+                            uint32_t n, uint8_t* digests_out);
+
+/* ------------------------------------------- benchmark / test utility only */
+/* Device-side synthetic request stream, byte-identical to the
+ * oracle generator: request i = LE64(i%16) || LE64(i/16) || data_len bytes of
+ * splitmix64(splitmix64(seed ^ i) + j).  count messages packed densely. */
+int mirsha_synth_requests_device(mirsha_ctx* ctx, uint64_t seed, uint64_t first, uint64_t count,
+                                 uint32_t data_len, uint8_t* d_arena);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIRSHA_H */

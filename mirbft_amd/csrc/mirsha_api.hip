@@ -1,0 +1,582 @@
+// mirsha_api.hip — host side of the C-ABI declared in include/mirsha.h.
+//
+// Owns device/pinned buffers (grow-only pools), the launch stream, length
+// bucketing and request-range sharding.  Every entry point returns digests in
+// ORIGIN order (processor.go:139 indexes Digests[i] by the request's position),
+// unlike ProcessorWorkPool's completion-order collector (processor.go:349-356).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/mirsha.h"
+#include "mirsha_kernels.h"
+#include "sha256_device.h"
+
+namespace {
+
+constexpr uint64_t kPackWindow = 256ull << 20;  // bytes per packed H2D chunk
+constexpr uint64_t kArenaSlack = 256;           // loader may touch up to 80 B past a message
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = std::max(n, cap + cap / 2);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            e = hipMalloc(&p, n);
+            if (e != hipSuccess) { p = nullptr; return e; }
+            want = n;
+        }
+        cap = want;
+        return hipSuccess;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        if (e != hipSuccess) { p = nullptr; return e; }
+        cap = n;
+        return hipSuccess;
+    }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+    void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
+};
+
+struct KernelTimer {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<hipEvent_t> pool;
+    uint64_t launches = 0;
+    double ms = 0.0;
+};
+
+}  // namespace
+
+struct mirsha_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    int variant = mirsha::kVariantLds;
+    bool timing = false;
+    std::string err;
+    DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2;
+    PinnedBuf h_stage;
+    KernelTimer timers[3];
+};
+
+namespace {
+
+int fail(mirsha_ctx* c, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIP_TRY(c, expr)                                                                    \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            return fail((c), _e == hipErrorOutOfMemory ? MIRSHA_ENOMEM : MIRSHA_EHIP,       \
+                        "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__, __LINE__); \
+    } while (0)
+
+hipEvent_t take_event(KernelTimer& t) {
+    if (!t.pool.empty()) {
+        hipEvent_t e = t.pool.back();
+        t.pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Brackets one launch with events on the launch stream when timing is on.
+template <class F>
+int timed_launch(mirsha_ctx* c, int which, F&& launch) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) {
+        e0 = take_event(c->timers[which]);
+        e1 = take_event(c->timers[which]);
+        if (e0) (void)hipEventRecord(e0, c->stream);
+    }
+    hipError_t e = launch();
+    if (e != hipSuccess) return fail(c, MIRSHA_EHIP, "kernel launch: %s", hipGetErrorString(e));
+    if (c->timing && e0 && e1) {
+        (void)hipEventRecord(e1, c->stream);
+        c->timers[which].pending.emplace_back(e0, e1);
+    }
+    return MIRSHA_OK;
+}
+
+int use_device(mirsha_ctx* c) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    return MIRSHA_OK;
+}
+
+uint32_t host_blocks(uint32_t L) { return (uint32_t)(((uint64_t)L + 72u) >> 6); }
+
+// Stable sort of message indices by block count, longest first.
+bool bucket_order(const uint32_t* len, uint32_t n, uint32_t* order) {
+    if (n == 0) return true;
+    uint32_t lo = UINT32_MAX, hi = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t b = host_blocks(len[i]);
+        lo = std::min(lo, b);
+        hi = std::max(hi, b);
+    }
+    if (lo == hi) {
+        for (uint32_t i = 0; i < n; i++) order[i] = i;
+        return true;
+    }
+    const uint64_t range = (uint64_t)hi - lo + 1;
+    if (range <= (1u << 22)) {
+        std::vector<uint32_t> count(range + 1, 0);
+        for (uint32_t i = 0; i < n; i++) count[hi - host_blocks(len[i]) + 1]++;
+        for (uint64_t k = 1; k <= range; k++) count[k] += count[k - 1];
+        for (uint32_t i = 0; i < n; i++) order[count[hi - host_blocks(len[i])]++] = i;
+    } else {
+        for (uint32_t i = 0; i < n; i++) order[i] = i;
+        std::stable_sort(order, order + n, [&](uint32_t a, uint32_t b) {
+            return host_blocks(len[a]) > host_blocks(len[b]);
+        });
+    }
+    return false;
+}
+
+// Hash n messages whose bytes are in device memory at d_arena (offsets
+// relative to it), writing digests to d_out (device, origin order).
+int hash_resident(mirsha_ctx* c, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* h_off,
+                  const uint32_t* h_len, uint32_t n, uint8_t* d_out) {
+    HIP_TRY(c, c->d_off.ensure(sizeof(uint64_t) * n));
+    HIP_TRY(c, c->d_len.ensure(sizeof(uint32_t) * n));
+    std::vector<uint32_t> order(n);
+    const bool identity = bucket_order(h_len, n, order.data());
+    HIP_TRY(c, hipMemcpyAsync(c->d_off.p, h_off, sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_len.p, h_len, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream));
+    const uint32_t* d_order = nullptr;
+    if (!identity) {
+        HIP_TRY(c, c->d_order.ensure(sizeof(uint32_t) * n));
+        HIP_TRY(c, hipMemcpyAsync(c->d_order.p, order.data(), sizeof(uint32_t) * n,
+                                  hipMemcpyHostToDevice, c->stream));
+        d_order = c->d_order.as<uint32_t>();
+    }
+    int rc = timed_launch(c, 0, [&] {
+        return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, c->d_off.as<uint64_t>(),
+                                   c->d_len.as<uint32_t>(), d_order, n, d_out, c->variant, c->stream);
+    });
+    if (rc) return rc;
+    // The host vectors above must outlive the async copies.
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+// Digests of n host messages into device buffer d_out (n*32 bytes).
+// Copies the arena span directly when it is dense, otherwise packs messages
+// into pinned staging windows.
+int hash_host_messages(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                       const uint32_t* len, uint32_t n, uint8_t* d_out) {
+    if (n == 0) return MIRSHA_OK;
+    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (len[i] > MIRSHA_MAX_MESSAGE_BYTES)
+            return fail(c, MIRSHA_ERANGE, "message %u is %u bytes (max %u)", i, len[i], MIRSHA_MAX_MESSAGE_BYTES);
+        if (off[i] > arena_len || len[i] > arena_len - off[i])
+            return fail(c, MIRSHA_EINVAL, "message %u [%llu,+%u) outside arena of %llu bytes", i,
+                        (unsigned long long)off[i], len[i], (unsigned long long)arena_len);
+        lo = std::min<uint64_t>(lo, off[i]);
+        hi = std::max<uint64_t>(hi, off[i] + len[i]);
+        total += len[i];
+    }
+    const uint64_t span = hi - lo;
+    if (span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES && span <= 2 * total + 4096) {
+        // Dense: one H2D copy of the span, offsets rebased.
+        HIP_TRY(c, c->d_arena.ensure(span + kArenaSlack));
+        if (span)
+            HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, arena + lo, span, hipMemcpyHostToDevice, c->stream));
+        std::vector<uint64_t> roff(off, off + n);
+        if (lo)
+            for (auto& x : roff) x -= lo;
+        return hash_resident(c, c->d_arena.as<uint8_t>(), span, roff.data(), len, n, d_out);
+    }
+    // Sparse or huge: pack consecutive messages into windows.
+    uint32_t i = 0;
+    while (i < n) {
+        uint64_t bytes = 0;
+        uint32_t j = i;
+        while (j < n && (j == i || bytes + len[j] <= kPackWindow)) bytes += len[j++];
+        HIP_TRY(c, c->h_stage.ensure(bytes + kArenaSlack));
+        HIP_TRY(c, c->d_arena.ensure(bytes + kArenaSlack));
+        std::vector<uint64_t> poff(j - i);
+        uint64_t p = 0;
+        uint8_t* st = c->h_stage.as<uint8_t>();
+        for (uint32_t k = i; k < j; k++) {
+            poff[k - i] = p;
+            if (len[k]) memcpy(st + p, arena + off[k], len[k]);
+            p += len[k];
+        }
+        if (bytes)
+            HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, st, bytes, hipMemcpyHostToDevice, c->stream));
+        int rc = hash_resident(c, c->d_arena.as<uint8_t>(), bytes, poff.data(), len + i, j - i,
+                               d_out + 32ull * i);
+        if (rc) return rc;
+        i = j;
+    }
+    return MIRSHA_OK;
+}
+
+int check_lists(mirsha_ctx* c, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
+                uint32_t n_digests) {
+    if (!first) return fail(c, MIRSHA_EINVAL, "list_first is NULL");
+    if (first[0] != 0) return fail(c, MIRSHA_EINVAL, "list_first[0] must be 0");
+    for (uint32_t b = 0; b < n_lists; b++)
+        if (first[b + 1] < first[b]) return fail(c, MIRSHA_EINVAL, "list_first not monotone at %u", b);
+    const uint32_t entries = first[n_lists];
+    if (entries && !idx) return fail(c, MIRSHA_EINVAL, "idx is NULL");
+    for (uint32_t e = 0; e < entries; e++)
+        if (idx[e] != MIRSHA_NULL_INDEX && idx[e] >= n_digests)
+            return fail(c, MIRSHA_EINVAL, "idx[%u]=%u out of range (%u digests)", e, idx[e], n_digests);
+    // 32 bytes per digest must fit a 32-bit message length.
+    for (uint32_t b = 0; b < n_lists; b++)
+        if ((uint64_t)(first[b + 1] - first[b]) * 32u > MIRSHA_MAX_MESSAGE_BYTES)
+            return fail(c, MIRSHA_ERANGE, "list %u too long", b);
+    return MIRSHA_OK;
+}
+
+// Digest lists over device-resident digests d_digests; writes d_out (device).
+int lists_resident(mirsha_ctx* c, const uint8_t* d_digests, const uint32_t* idx,
+                   const uint32_t* first, uint32_t n_lists, uint8_t* d_out) {
+    const uint32_t entries = first[n_lists];
+    HIP_TRY(c, c->d_first.ensure(sizeof(uint32_t) * (n_lists + 1)));
+    HIP_TRY(c, c->d_idx.ensure(sizeof(uint32_t) * std::max<uint32_t>(entries, 1)));
+    HIP_TRY(c, hipMemcpyAsync(c->d_first.p, first, sizeof(uint32_t) * (n_lists + 1), hipMemcpyHostToDevice, c->stream));
+    if (entries)
+        HIP_TRY(c, hipMemcpyAsync(c->d_idx.p, idx, sizeof(uint32_t) * entries, hipMemcpyHostToDevice, c->stream));
+    return timed_launch(c, 1, [&] {
+        return mirsha::launch_lists(d_digests, c->d_idx.as<uint32_t>(), c->d_first.as<uint32_t>(),
+                                    n_lists, d_out, c->stream);
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int mirsha_version(void) { return (0 << 16) | 1; }
+
+int mirsha_device_count(int* count) {
+    if (!count) return MIRSHA_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        n = 0;
+    }
+    *count = n;
+    return MIRSHA_OK;
+}
+
+int mirsha_ctx_create(int device, mirsha_ctx** out) {
+    if (!out) return MIRSHA_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return MIRSHA_ENODEV;
+    }
+    if (device < 0 || device >= n) return MIRSHA_EINVAL;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return MIRSHA_EHIP;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return MIRSHA_ENODEV;  // gfx950 code objects only
+    mirsha_ctx* c = new mirsha_ctx();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return MIRSHA_EHIP;
+    }
+    c->stream = c->own;
+    *out = c;
+    return MIRSHA_OK;
+}
+
+void mirsha_ctx_destroy(mirsha_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& t : c->timers) {
+        for (auto& pr : t.pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+        for (auto e : t.pool) (void)hipEventDestroy(e);
+    }
+    c->d_arena.release(); c->d_off.release(); c->d_len.release(); c->d_order.release();
+    c->d_out.release(); c->d_idx.release(); c->d_first.release(); c->d_out2.release();
+    c->h_stage.release();
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+const char* mirsha_last_error(const mirsha_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mirsha_ctx_set_stream(mirsha_ctx* c, void* s) {
+    if (!c) return MIRSHA_EINVAL;
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own;
+    return MIRSHA_OK;
+}
+
+void* mirsha_ctx_stream(mirsha_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int mirsha_ctx_set_variant(mirsha_ctx* c, int v) {
+    if (!c || (v != mirsha::kVariantLds && v != mirsha::kVariantDirect)) return MIRSHA_EINVAL;
+    c->variant = v;
+    return MIRSHA_OK;
+}
+
+int mirsha_ctx_set_timing(mirsha_ctx* c, int enable) {
+    if (!c) return MIRSHA_EINVAL;
+    c->timing = enable != 0;
+    return MIRSHA_OK;
+}
+
+int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double* total_ms) {
+    if (!c || which < 0 || which > 2) return MIRSHA_EINVAL;
+    if (int rc = use_device(c)) return rc;
+    KernelTimer& t = c->timers[which];
+    for (auto& pr : t.pending) {
+        HIP_TRY(c, hipEventSynchronize(pr.second));
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+        t.ms += ms;
+        t.launches++;
+        t.pool.push_back(pr.first);
+        t.pool.push_back(pr.second);
+    }
+    t.pending.clear();
+    if (launches) *launches = t.launches;
+    if (total_ms) *total_ms = t.ms;
+    return MIRSHA_OK;
+}
+
+int mirsha_ctx_reset_timing(mirsha_ctx* c) {
+    if (!c) return MIRSHA_EINVAL;
+    for (int k = 0; k < 3; k++) {
+        int rc = mirsha_ctx_kernel_time(c, k, nullptr, nullptr);
+        if (rc) return rc;
+        c->timers[k].launches = 0;
+        c->timers[k].ms = 0.0;
+    }
+    return MIRSHA_OK;
+}
+
+int mirsha_sync(mirsha_ctx* c) {
+    if (!c) return MIRSHA_EINVAL;
+    if (int rc = use_device(c)) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_hash_batch(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                      const uint32_t* len, uint32_t n, uint8_t* out) {
+    if (!c) return MIRSHA_EINVAL;
+    if (n == 0) return MIRSHA_OK;
+    if (!off || !len || !out || (!arena && arena_len)) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (int rc = use_device(c)) return rc;
+    HIP_TRY(c, c->d_out.ensure(32ull * n));
+    if (int rc = hash_host_messages(c, arena, arena_len, off, len, n, c->d_out.as<uint8_t>())) return rc;
+    HIP_TRY(c, hipMemcpyAsync(out, c->d_out.p, 32ull * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                       const uint32_t* slice_first, uint32_t n, uint8_t* out) {
+    if (!c) return MIRSHA_EINVAL;
+    if (n == 0) return MIRSHA_OK;
+    if (!slice_first || !out) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (slice_first[0] != 0) return fail(c, MIRSHA_EINVAL, "slice_first[0] must be 0");
+    const uint32_t ns = slice_first[n];
+    if (ns && (!slice_ptr || !slice_len)) return fail(c, MIRSHA_EINVAL, "NULL slice arrays");
+    std::vector<uint64_t> off(n);
+    std::vector<uint32_t> len(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (slice_first[i + 1] < slice_first[i]) return fail(c, MIRSHA_EINVAL, "slice_first not monotone");
+        uint64_t L = 0;
+        for (uint32_t s = slice_first[i]; s < slice_first[i + 1]; s++) {
+            if (slice_len[s] && !slice_ptr[s]) return fail(c, MIRSHA_EINVAL, "slice %u is NULL", s);
+            L += slice_len[s];
+        }
+        if (L > MIRSHA_MAX_MESSAGE_BYTES) return fail(c, MIRSHA_ERANGE, "request %u is %llu bytes", i, (unsigned long long)L);
+        off[i] = total;
+        len[i] = (uint32_t)L;
+        total += L;
+    }
+    if (int rc = use_device(c)) return rc;
+    // One packing pass into pinned memory (the Go side's single copy), then the
+    // common path; windows bound the staging footprint.
+    HIP_TRY(c, c->d_out.ensure(32ull * n));
+    uint32_t i = 0;
+    while (i < n) {
+        uint64_t bytes = 0;
+        uint32_t j = i;
+        while (j < n && (j == i || bytes + len[j] <= kPackWindow)) bytes += len[j++];
+        HIP_TRY(c, c->h_stage.ensure(bytes + kArenaSlack));
+        HIP_TRY(c, c->d_arena.ensure(bytes + kArenaSlack));
+        uint8_t* st = c->h_stage.as<uint8_t>();
+        std::vector<uint64_t> poff(j - i);
+        uint64_t p = 0;
+        for (uint32_t k = i; k < j; k++) {
+            poff[k - i] = p;
+            for (uint32_t s = slice_first[k]; s < slice_first[k + 1]; s++) {
+                if (slice_len[s]) memcpy(st + p, slice_ptr[s], slice_len[s]);
+                p += slice_len[s];
+            }
+        }
+        if (bytes)
+            HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, st, bytes, hipMemcpyHostToDevice, c->stream));
+        if (int rc = hash_resident(c, c->d_arena.as<uint8_t>(), bytes, poff.data(), len.data() + i, j - i,
+                                   c->d_out.as<uint8_t>() + 32ull * i))
+            return rc;
+        i = j;
+    }
+    HIP_TRY(c, hipMemcpyAsync(out, c->d_out.p, 32ull * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len,
+                                      const uint64_t* off, const uint32_t* len, uint32_t n_req,
+                                      const uint32_t* idx, const uint32_t* first, uint32_t n_batches,
+                                      uint8_t* req_out, uint8_t* batch_out) {
+    if (!c) return MIRSHA_EINVAL;
+    if (n_req && (!off || !len || !req_out || (!arena && arena_len))) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (n_batches && !batch_out) return fail(c, MIRSHA_EINVAL, "batch_digests_out is NULL");
+    if (n_batches)
+        if (int rc = check_lists(c, idx, first, n_batches, n_req)) return rc;
+    if (int rc = use_device(c)) return rc;
+    HIP_TRY(c, c->d_out.ensure(32ull * std::max<uint32_t>(n_req, 1)));
+    if (int rc = hash_host_messages(c, arena, arena_len, off, len, n_req, c->d_out.as<uint8_t>())) return rc;
+    if (n_batches) {
+        HIP_TRY(c, c->d_out2.ensure(32ull * n_batches));
+        if (int rc = lists_resident(c, c->d_out.as<uint8_t>(), idx, first, n_batches, c->d_out2.as<uint8_t>()))
+            return rc;
+        HIP_TRY(c, hipMemcpyAsync(batch_out, c->d_out2.p, 32ull * n_batches, hipMemcpyDeviceToHost, c->stream));
+    }
+    if (n_req) HIP_TRY(c, hipMemcpyAsync(req_out, c->d_out.p, 32ull * n_req, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digests, const uint32_t* idx,
+                        const uint32_t* first, uint32_t n_lists, uint8_t* out) {
+    if (!c) return MIRSHA_EINVAL;
+    if (n_lists == 0) return MIRSHA_OK;
+    if (!out || (n_digests && !digests)) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (int rc = check_lists(c, idx, first, n_lists, n_digests)) return rc;
+    if (int rc = use_device(c)) return rc;
+    HIP_TRY(c, c->d_arena.ensure(32ull * std::max<uint32_t>(n_digests, 1)));
+    if (n_digests)
+        HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, digests, 32ull * n_digests, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, c->d_out2.ensure(32ull * n_lists));
+    if (int rc = lists_resident(c, c->d_arena.as<uint8_t>(), idx, first, n_lists, c->d_out2.as<uint8_t>())) return rc;
+    HIP_TRY(c, hipMemcpyAsync(out, c->d_out2.p, 32ull * n_lists, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_hash_batch_device(mirsha_ctx* c, const uint8_t* d_arena, uint64_t arena_len,
+                             const uint64_t* d_off, const uint32_t* d_len, const uint32_t* d_order,
+                             uint32_t n, uint8_t* d_out) {
+    if (!c) return MIRSHA_EINVAL;
+    if (n == 0) return MIRSHA_OK;
+    if (!d_off || !d_len || !d_out || (!d_arena && arena_len)) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (arena_len > MIRSHA_MAX_DEVICE_ARENA_BYTES)
+        return fail(c, MIRSHA_ERANGE, "device arena %llu bytes > %u", (unsigned long long)arena_len,
+                    MIRSHA_MAX_DEVICE_ARENA_BYTES);
+    if (int rc = use_device(c)) return rc;
+    return timed_launch(c, 0, [&] {
+        return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, d_off, d_len, d_order, n, d_out, c->variant,
+                                   c->stream);
+    });
+}
+
+int mirsha_digest_lists_device(mirsha_ctx* c, const uint8_t* d_digests, const uint32_t* d_idx,
+                               const uint32_t* d_first, uint32_t n_lists, uint8_t* d_out) {
+    if (!c) return MIRSHA_EINVAL;
+    if (n_lists == 0) return MIRSHA_OK;
+    if (!d_digests || !d_idx || !d_first || !d_out) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (int rc = use_device(c)) return rc;
+    return timed_launch(c, 1, [&] { return mirsha::launch_lists(d_digests, d_idx, d_first, n_lists, d_out, c->stream); });
+}
+
+int mirsha_bucket_order(const uint32_t* len, uint32_t n, uint32_t* order_out) {
+    if (n && (!len || !order_out)) return MIRSHA_EINVAL;
+    return bucket_order(len, n, order_out) ? 1 : 0;
+}
+
+int mirsha_synth_requests_device(mirsha_ctx* c, uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
+                                 uint8_t* d_arena) {
+    if (!c) return MIRSHA_EINVAL;
+    if (count && !d_arena) return fail(c, MIRSHA_EINVAL, "NULL arena");
+    if (int rc = use_device(c)) return rc;
+    return timed_launch(c, 2, [&] { return mirsha::launch_gen_requests(seed, first, count, data_len, d_arena, c->stream); });
+}
+
+int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena, uint64_t arena_len,
+                            const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* out) {
+    if (ndev <= 0 || !devices) return MIRSHA_EINVAL;
+    if (n == 0) return MIRSHA_OK;
+    if (!off || !len || !out) return MIRSHA_EINVAL;
+    // Contiguous request ranges balanced by compressions.
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += host_blocks(len[i]);
+    std::vector<uint32_t> cut(ndev + 1, n);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    int d = 1;
+    for (uint32_t i = 0; i < n && d < ndev; i++) {
+        acc += host_blocks(len[i]);
+        while (d < ndev && acc * ndev >= total * (uint64_t)d) cut[d++] = i + 1;
+    }
+    std::vector<int> rcs(ndev, MIRSHA_OK);
+    std::vector<std::thread> th;
+    for (int k = 0; k < ndev; k++) {
+        th.emplace_back([&, k] {
+            const uint32_t a = cut[k], b = cut[k + 1];
+            if (a >= b) return;
+            mirsha_ctx* c = nullptr;
+            int rc = mirsha_ctx_create(devices[k], &c);
+            if (rc == MIRSHA_OK) rc = mirsha_hash_batch(c, arena, arena_len, off + a, len + a, b - a, out + 32ull * a);
+            rcs[k] = rc;
+            mirsha_ctx_destroy(c);
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int k = 0; k < ndev; k++)
+        if (rcs[k]) return rcs[k];
+    return MIRSHA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,22 @@
+// mirsha_kernels.h — internal launcher declarations (not part of the C-ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mirsha {
+
+constexpr uint32_t kWavesPerBlock = 4;
+constexpr uint32_t kBlockThreads = 64 * kWavesPerBlock;
+constexpr uint32_t kNullIndex = 0xFFFFFFFFu;
+
+enum : int { kVariantLds = 0, kVariantDirect = 1 };
+
+hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t* off,
+                       const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
+                       int variant, hipStream_t s);
+hipError_t launch_lists(const uint8_t* digests, const uint32_t* idx, const uint32_t* first,
+                        uint32_t n_lists, uint8_t* out, hipStream_t s);
+hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
+                               uint8_t* arena, hipStream_t s);
+
+}  // namespace mirsha

@@ -1,0 +1,256 @@
+// mirsha_kernels.hip — gfx950 kernels for MirBFT's Actions.Hash hot path.
+//
+//   sha256_msgs_kernel    request / generic messages packed in an arena
+//                         (processor.go:129-143; one lane = one HashRequest)
+//   sha256_lists_kernel   dependent second pass: digest of an ordered list of
+//                         device-resident 32-byte digests (batch digests,
+//                         sequence.go:154-157; VerifyBatch, batch_tracker.go:147-150;
+//                         checkpoint chain, testengine/recorder.go:213-256)
+//   gen_requests_kernel   synthetic request stream (bench/test utility, §8d)
+//
+// Layout: one wave (64 lanes) owns a tile of 64 messages, lane = message.
+// In the LDS-staged form every lane is also a loader: per block, lane
+// (j, q) = (lane>>2 + 16j, lane&3) fetches the 16-byte quarter q of message
+// 16j + lane>>2 — 16 messages x 64 contiguous bytes per wave instruction —
+// assembles big-endian words with one v_perm_b32 each, applies FIPS padding
+// on the tail chunks, and writes them into the wave's private 4 KiB LDS tile,
+// XOR-swizzled so both the ds_write_b128 (8-lane groups, 128 contiguous bytes)
+// and the per-lane ds_read_b128 (16-lane groups) are bank-conflict free.
+#include "mirsha_kernels.h"
+#include "sha256_device.h"
+
+namespace mirsha {
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64);
+        v = v > o ? v : o;
+    }
+    return v;
+}
+
+// 16-byte chunk q of block blk of a message at arena offset o, length L,
+// as 4 big-endian SHA words with padding applied.
+__device__ __forceinline__ void load_chunk(__amdgpu_buffer_rsrc_t rsrc, uint32_t o, uint32_t L,
+                                           uint32_t blk, uint32_t q, bool last_block,
+                                           uint32_t out[4]) {
+    const uint32_t p = 64u * blk + 16u * q;
+    const uint32_t addr = o + p;
+    const uint32_t a = addr & ~3u;
+    const uint32_t sel = be_sel(addr & 3u);
+    // Raw buffer loads: range-checked against the arena length, so reads past
+    // the arena end return 0 instead of faulting.
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a, 0, 0);
+    const uint32_t v4 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
+    out[0] = be_word(v[1], v[0], sel);
+    out[1] = be_word(v[2], v[1], sel);
+    out[2] = be_word(v[3], v[2], sel);
+    out[3] = be_word(v4, v[3], sel);
+    if (p + 16u > L) pad_chunk(out, p, L, last_block, q);
+}
+
+// Swizzled 16-byte slot of (message m, quarter q) inside a wave's 256-slot tile.
+__device__ __forceinline__ uint32_t lds_slot(uint32_t m, uint32_t q) {
+    return m * 4u + (q ^ ((m >> 2) & 3u));
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* out, uint32_t msg, const uint32_t st[8]) {
+    uint4* d = reinterpret_cast<uint4*>(out + 32ull * msg);
+    d[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                      __builtin_bswap32(st[3]));
+    d[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                      __builtin_bswap32(st[7]));
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
+    const uint8_t* __restrict__ arena, uint32_t arena_len, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
+    uint8_t* __restrict__ out) {
+    __shared__ uint4 tile[kWavesPerBlock][256];
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * kWavesPerBlock + wv;
+    const uint32_t slot = t * 64u + lane;
+    if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
+
+    const bool valid = slot < n;
+    const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
+    const uint32_t L = valid ? len[msg] : 0u;
+    const uint32_t o = valid ? (uint32_t)off[msg] : 0u;
+    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
+    const uint32_t wave_nb = wave_max(nb);
+
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)arena_len, 0x00020000);
+
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+
+    if constexpr (kLds) {
+        // Loader roles: this lane fetches quarter q of messages m_j = 16j + lane/4.
+        const uint32_t q = lane & 3u;
+        uint32_t Lj[4], oj[4], nbj[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int src = 16 * j + (int)(lane >> 2);
+            Lj[j] = (uint32_t)__shfl((int)L, src, 64);
+            oj[j] = (uint32_t)__shfl((int)o, src, 64);
+            nbj[j] = (uint32_t)__shfl((int)nb, src, 64);
+        }
+        uint4* my = tile[wv];
+        for (uint32_t blk = 0; blk < wave_nb; blk++) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (blk < nbj[j]) {
+                    uint32_t wq[4];
+                    load_chunk(rsrc, oj[j], Lj[j], blk, q, blk + 1u == nbj[j], wq);
+                    my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+                }
+            }
+            // Cross-lane hand-off inside one wave: LDS ops of a wave execute in
+            // order; the fence only stops the compiler from reordering them.
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+                w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (blk < nb) compress(st, w);
+        }
+    } else {
+        for (uint32_t blk = 0; blk < wave_nb; blk++) {
+            if (blk < nb) {
+                uint32_t w[16];
+                const bool last = blk + 1u == nb;
+#pragma unroll
+                for (int q = 0; q < 4; q++) load_chunk(rsrc, o, L, blk, (uint32_t)q, last, &w[4 * q]);
+                compress(st, w);
+            }
+        }
+    }
+    if (valid) store_digest(out, msg, st);
+}
+
+// Dependent pass: message k = concat(digests[idx[e]] for e in [first[k], first[k+1]))
+// skipping idx == kNullIndex (a null request's empty digest, client_tracker.go:840-847).
+__global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
+    const uint8_t* __restrict__ digests, const uint32_t* __restrict__ idx,
+    const uint32_t* __restrict__ first, uint32_t n_lists, uint8_t* __restrict__ out) {
+    const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
+    const bool valid = k < n_lists;
+    const uint32_t e0 = valid ? first[k] : 0u;
+    const uint32_t e1 = valid ? first[k + 1] : 0u;
+    uint32_t c = 0;  // non-null entries
+    for (uint32_t e = e0; e < e1; e++) c += idx[e] != kNullIndex;
+    const uint32_t L = 32u * c;
+    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
+    const uint32_t wave_nb = wave_max(nb);
+
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    uint32_t cur = e0;  // cursor over the index list
+    for (uint32_t blk = 0; blk < wave_nb; blk++) {
+        if (blk < nb) {
+            uint32_t w[16];
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+                const uint32_t di = 2u * blk + (uint32_t)half;  // digest ordinal in the message
+                if (di < c) {
+                    while (idx[cur] == kNullIndex) cur++;
+                    const uint4* src = reinterpret_cast<const uint4*>(digests + 32ull * idx[cur]);
+                    cur++;
+                    const uint4 x0 = src[0], x1 = src[1];
+                    w[8 * half + 0] = __builtin_bswap32(x0.x); w[8 * half + 1] = __builtin_bswap32(x0.y);
+                    w[8 * half + 2] = __builtin_bswap32(x0.z); w[8 * half + 3] = __builtin_bswap32(x0.w);
+                    w[8 * half + 4] = __builtin_bswap32(x1.x); w[8 * half + 5] = __builtin_bswap32(x1.y);
+                    w[8 * half + 6] = __builtin_bswap32(x1.z); w[8 * half + 7] = __builtin_bswap32(x1.w);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) w[8 * half + i] = 0u;
+                    if (di == c) w[8 * half] = 0x80000000u;
+                }
+            }
+            if (blk + 1u == nb) {
+                w[14] = L >> 29;
+                w[15] = L << 3;
+            }
+            compress(st, w);
+        }
+    }
+    if (valid) store_digest(out, k, st);
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Same stream as oracle_gen_requests (oracle/sha256_oracle.c): one thread per
+// 8-byte word of the packed (16 + data_len)-byte messages.
+__global__ void gen_requests_kernel(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
+                                    uint8_t* __restrict__ arena) {
+    const uint64_t stride = 16ull + data_len;
+    const uint64_t words_per_msg = (data_len + 7u) / 8u + 2u;
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= count * words_per_msg) return;
+    const uint64_t r = gid / words_per_msg, wi = gid % words_per_msg;
+    const uint64_t i = first + r;
+    uint8_t* m = arena + r * stride;
+    uint64_t v;
+    uint32_t nbytes = 8, base;
+    if (wi == 0) { v = i % 16u; base = 0; }
+    else if (wi == 1) { v = i / 16u; base = 8; }
+    else {
+        const uint32_t j = (uint32_t)(wi - 2);
+        v = splitmix64(splitmix64(seed ^ i) + j);
+        base = 16u + 8u * j;
+        if (8u * j + 8u > data_len) nbytes = data_len - 8u * j;
+    }
+    for (uint32_t b = 0; b < nbytes; b++) m[base + b] = (uint8_t)(v >> (8 * b));
+}
+
+// ---- host-side launchers --------------------------------------------------
+hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t* off,
+                       const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
+                       int variant, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t tiles = (n + 63u) / 64u;
+    const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
+    if (variant == kVariantDirect)
+        sha256_msgs_kernel<false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+    else
+        sha256_msgs_kernel<true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_lists(const uint8_t* digests, const uint32_t* idx, const uint32_t* first,
+                        uint32_t n_lists, uint8_t* out, hipStream_t s) {
+    if (n_lists == 0) return hipSuccess;
+    const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
+    sha256_lists_kernel<<<grid, kBlockThreads, 0, s>>>(digests, idx, first, n_lists, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
+                               uint8_t* arena, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const uint64_t words = count * ((data_len + 7u) / 8u + 2u);
+    const uint64_t grid = (words + 255u) / 256u;
+    gen_requests_kernel<<<(unsigned)grid, 256, 0, s>>>(seed, first, count, data_len, arena);
+    return hipGetLastError();
+}
+
+}  // namespace mirsha

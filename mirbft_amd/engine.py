@@ -1,0 +1,227 @@
+"""Engine: one gfx950 device context behind the C-ABI (include/mirsha.h).
+
+Host-memory entry points take numpy arrays / bytes and return numpy digests
+``(n, 32) uint8`` in ORIGIN order.  Device-pointer entry points take raw device
+addresses (ints, e.g. ``torch.Tensor.data_ptr()``) and are asynchronous on the
+engine's stream.  Every call runs the HIP kernels; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import MIRSHA_NULL_INDEX, MirshaError, check
+
+KERNEL_MSGS = 0
+KERNEL_LISTS = 1
+KERNEL_GEN = 2
+VARIANT_LDS = 0
+VARIANT_DIRECT = 1
+
+
+def _ptr(a: np.ndarray | None) -> int | None:
+    if a is None:
+        return None
+    return a.ctypes.data if a.size else None
+
+
+def _as_u8(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf.reshape(-1).view(np.uint8))
+    return np.frombuffer(memoryview(buf), dtype=np.uint8)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(_lib.load().mirsha_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Engine:
+    """Batched SHA-256 engine on one MI355X.  Replaces `Hasher` (processor.go:21)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = _lib.load()
+        ctx = ctypes.c_void_p()
+        rc = self._lib.mirsha_ctx_create(int(device), ctypes.byref(ctx))
+        if rc != 0:
+            raise MirshaError(rc, f"cannot create a gfx950 context on device {device}")
+        self.ctx = ctx
+        self.device = device
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self) -> None:
+        if getattr(self, "ctx", None):
+            self._lib.mirsha_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int) -> None:
+        check(rc, self.ctx)
+
+    # --------------------------------------------------------------- knobs
+    def set_stream(self, stream_ptr: int | None) -> None:
+        self._check(self._lib.mirsha_ctx_set_stream(self.ctx, stream_ptr))
+
+    @property
+    def stream(self) -> int:
+        return self._lib.mirsha_ctx_stream(self.ctx) or 0
+
+    def set_variant(self, variant: int) -> None:
+        self._check(self._lib.mirsha_ctx_set_variant(self.ctx, int(variant)))
+
+    def set_timing(self, enable: bool) -> None:
+        self._check(self._lib.mirsha_ctx_set_timing(self.ctx, 1 if enable else 0))
+
+    def kernel_time(self, kernel: int) -> tuple[int, float]:
+        n = ctypes.c_uint64(0)
+        ms = ctypes.c_double(0.0)
+        self._check(self._lib.mirsha_ctx_kernel_time(self.ctx, int(kernel), ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    def reset_timing(self) -> None:
+        self._check(self._lib.mirsha_ctx_reset_timing(self.ctx))
+
+    def sync(self) -> None:
+        self._check(self._lib.mirsha_sync(self.ctx))
+
+    # ------------------------------------------------------------ host API
+    def hash_batch(self, arena, off: Sequence[int], length: Sequence[int]) -> np.ndarray:
+        """Digest of arena[off[i]:off[i]+len[i]] for every i (processor.go:133-143)."""
+        a = _as_u8(arena)
+        o = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(length, dtype=np.uint32)
+        if o.shape != ln.shape:
+            raise ValueError("off and len differ in length")
+        n = int(o.size)
+        out = np.empty((n, 32), dtype=np.uint8)
+        if n:
+            self._check(self._lib.mirsha_hash_batch(self.ctx, _ptr(a), a.size, _ptr(o), _ptr(ln), n, _ptr(out)))
+        return out
+
+    def hash_messages(self, messages: Sequence[bytes]) -> np.ndarray:
+        """One digest per message (each a single byte string)."""
+        lens = np.fromiter((len(m) for m in messages), dtype=np.uint32, count=len(messages))
+        off = np.zeros(len(messages), dtype=np.uint64)
+        if len(messages) > 1:
+            np.cumsum(lens[:-1], out=off[1:])
+        arena = b"".join(messages)
+        return self.hash_batch(arena, off, lens)
+
+    def hash_slices(self, requests: Sequence[Sequence[bytes]]) -> np.ndarray:
+        """Digest of concat(req) for each req = HashRequest.Data (actions.go:157-164)."""
+        n = len(requests)
+        out = np.empty((n, 32), dtype=np.uint8)
+        if n == 0:
+            return out
+        keep = []
+        ptrs, lens, first = [], [], [0]
+        for req in requests:
+            for s in req:
+                b = bytes(s)
+                keep.append(b)
+                lens.append(len(b))
+            first.append(len(keep))
+        ns = len(keep)
+        ptr_arr = (ctypes.c_void_p * max(ns, 1))()
+        for i, b in enumerate(keep):
+            ptr_arr[i] = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value if len(b) else None
+        len_arr = np.asarray(lens if ns else [0], dtype=np.uint64)
+        first_arr = np.asarray(first, dtype=np.uint32)
+        self._check(
+            self._lib.mirsha_hash_slices(self.ctx, ctypes.addressof(ptr_arr), _ptr(len_arr), _ptr(first_arr), n, _ptr(out))
+        )
+        return out
+
+    def hash_requests_then_batches(self, arena, off, length, idx, batch_first):
+        """Request digests, then batch digests over them on device (sequence.go:154-157)."""
+        a = _as_u8(arena)
+        o = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(length, dtype=np.uint32)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        fs = np.ascontiguousarray(batch_first, dtype=np.uint32)
+        n, nb = int(o.size), int(fs.size) - 1
+        if nb < 0:
+            raise ValueError("batch_first needs n_batches + 1 entries")
+        req = np.empty((n, 32), dtype=np.uint8)
+        bat = np.empty((nb, 32), dtype=np.uint8)
+        self._check(
+            self._lib.mirsha_hash_requests_then_batches(
+                self.ctx, _ptr(a), a.size, _ptr(o), _ptr(ln), n, _ptr(ix), _ptr(fs), nb, _ptr(req), _ptr(bat)
+            )
+        )
+        return req, bat
+
+    def digest_lists(self, digests, idx, list_first) -> np.ndarray:
+        """SHA-256 over ordered lists of 32-byte digests (batch / VerifyBatch / checkpoint chain)."""
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1, 32)
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        fs = np.ascontiguousarray(list_first, dtype=np.uint32)
+        nl = int(fs.size) - 1
+        out = np.empty((max(nl, 0), 32), dtype=np.uint8)
+        if nl > 0:
+            self._check(
+                self._lib.mirsha_digest_lists(self.ctx, _ptr(d), d.shape[0], _ptr(ix), _ptr(fs), nl, _ptr(out))
+            )
+        return out
+
+    # ---------------------------------------------------------- device API
+    def hash_batch_device(self, d_arena: int, arena_len: int, d_off: int, d_len: int, d_order: int | None,
+                          n: int, d_out: int) -> None:
+        self._check(self._lib.mirsha_hash_batch_device(self.ctx, d_arena, arena_len, d_off, d_len, d_order, n, d_out))
+
+    def digest_lists_device(self, d_digests: int, d_idx: int, d_first: int, n_lists: int, d_out: int) -> None:
+        self._check(self._lib.mirsha_digest_lists_device(self.ctx, d_digests, d_idx, d_first, n_lists, d_out))
+
+    def synth_requests_device(self, seed: int, first: int, count: int, data_len: int, d_arena: int) -> None:
+        self._check(self._lib.mirsha_synth_requests_device(self.ctx, seed, first, count, data_len, d_arena))
+
+
+def bucket_order(length: Sequence[int]) -> tuple[np.ndarray, bool]:
+    """Message order sorted by block count, longest first (stable); (order, is_identity)."""
+    ln = np.ascontiguousarray(length, dtype=np.uint32)
+    order = np.empty(ln.size, dtype=np.uint32)
+    rc = _lib.load().mirsha_bucket_order(_ptr(ln), ln.size, _ptr(order))
+    if rc < 0:
+        raise MirshaError(rc, "bucket_order")
+    return order, bool(rc == 1)
+
+
+def hash_batch_multi(devices: Iterable[int], arena, off, length) -> np.ndarray:
+    """Request-range sharding over several devices in one process; host gather."""
+    devs = np.ascontiguousarray(list(devices), dtype=np.int32)
+    a = _as_u8(arena)
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(length, dtype=np.uint32)
+    out = np.empty((o.size, 32), dtype=np.uint8)
+    rc = _lib.load().mirsha_hash_batch_multi(_ptr(devs), devs.size, _ptr(a), a.size, _ptr(o), _ptr(ln), o.size, _ptr(out))
+    check(rc)
+    return out
+
+
+__all__ = [
+    "Engine",
+    "bucket_order",
+    "device_count",
+    "hash_batch_multi",
+    "MIRSHA_NULL_INDEX",
+    "KERNEL_MSGS",
+    "KERNEL_LISTS",
+    "KERNEL_GEN",
+    "VARIANT_LDS",
+    "VARIANT_DIRECT",
+]

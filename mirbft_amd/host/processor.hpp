@@ -1,0 +1,99 @@
+// processor.hpp — C++ host mirror of the reference's Processor hash path
+// (Go package github.com/IBM/mirbft; no Go toolchain in this image, so the
+// host side above the C-ABI is C++, with the reference's names and semantics).
+//
+//   reference                                   here
+//   type Hasher func() hash.Hash  processor.go:21     mirbft::Hasher (factory of mirbft::Hash)
+//   HashRequest{Data [][]byte; Origin}  actions.go:157-164   mirbft::HashRequest
+//   HashResult{Digest; Request}         actions.go:224-230   mirbft::HashResult
+//   ActionResults{Digests; ...}         actions.go:218-221   mirbft::ActionResults
+//   (*Processor).Process hash loop      processor.go:129-143 mirbft::Processor::Process
+//
+// Processor::Process coalesces every HashRequest of one Ready() cycle into ONE
+// batched device call (mirsha_hash_slices) and returns Digests[i] for
+// actions.Hash[i] with the Request back-pointer, in origin order.  Failures
+// throw std::runtime_error — the reference panics (processor.go:75,81,85,91).
+#pragma once
+#include <array>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+struct mirsha_ctx;
+
+namespace mirbft {
+
+struct Bytes {
+    const uint8_t* data = nullptr;
+    size_t size = 0;
+};
+
+// Origin is opaque to the hasher (actions.go:152-156): carried, never read.
+struct HashRequest {
+    std::vector<Bytes> Data;
+    const void* Origin = nullptr;
+};
+
+struct HashResult {
+    std::array<uint8_t, 32> Digest{};
+    const HashRequest* Request = nullptr;
+};
+
+struct Actions {
+    std::vector<const HashRequest*> Hash;  // actions.go:24
+};
+
+struct ActionResults {
+    std::vector<HashResult> Digests;  // actions.go:219
+};
+
+// Streaming hash.Hash (Write/Sum/Reset) for single-message callers.
+class Hash {
+public:
+    virtual ~Hash() = default;
+    virtual void Write(const uint8_t* p, size_t n) = 0;
+    virtual std::array<uint8_t, 32> Sum() const = 0;
+    virtual void Reset() = 0;
+};
+using Hasher = std::function<std::unique_ptr<Hash>()>;
+
+// One gfx950 engine (device context); the batched replacement for Hasher.
+class GpuEngine {
+public:
+    explicit GpuEngine(int device = 0);
+    ~GpuEngine();
+    GpuEngine(const GpuEngine&) = delete;
+    GpuEngine& operator=(const GpuEngine&) = delete;
+
+    // Digests of reqs[i] (concat of its Data slices) at out[i], origin order.
+    void HashBatch(const std::vector<const HashRequest*>& reqs, std::vector<std::array<uint8_t, 32>>& out);
+    mirsha_ctx* ctx() { return ctx_; }
+
+private:
+    mirsha_ctx* ctx_ = nullptr;
+};
+
+// hash.Hash whose Sum runs on the GPU (buffers its writes).
+std::unique_ptr<Hash> NewGpuSha256(GpuEngine& engine);
+
+class Processor {
+public:
+    explicit Processor(GpuEngine& engine) : engine_(engine) {}
+    // processor.go:129-143, batched.
+    ActionResults Process(const Actions& actions);
+
+private:
+    GpuEngine& engine_;
+};
+
+}  // namespace mirbft
+
+extern "C" {
+// Small C entry for tests: hash n single-slice requests through
+// mirbft::Processor (exercises the C++ mirror end to end).
+int mirbft_host_process(int device, const uint8_t* const* data, const uint64_t* len, uint32_t n,
+                        uint8_t* digests_out, char* err, uint32_t err_len);
+}

@@ -1,0 +1,58 @@
+"""Request-range sharding across GPUs.
+
+Independent hash requests (actions.go:22-23) shard by contiguous request range;
+cuts fall on batch boundaries so each GPU's dependent batch-digest pass reads
+only its own device-resident request digests.  No collective: a host gather
+(concatenation in rank order) restores origin order.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+
+
+def blocks_for_len(length) -> np.ndarray:
+    """SHA-256 compressions per message: ceil((L + 9) / 64)."""
+    return (np.asarray(length, dtype=np.uint64) + 72) >> 6
+
+
+def shard_ranges(n_req: int, world: int, batch_size: int = 1,
+                 lengths: Optional[Sequence[int]] = None) -> list[tuple[int, int]]:
+    """[lo, hi) request range per rank, cut on multiples of ``batch_size``.
+
+    With ``lengths`` the cuts balance total compressions, else request counts.
+    """
+    if world <= 0:
+        raise ValueError("world must be positive")
+    if n_req <= 0:
+        return [(0, 0)] * world
+    bs = max(1, int(batch_size))
+    n_units = (n_req + bs - 1) // bs
+    if lengths is None:
+        w = np.full(n_units, bs, dtype=np.float64)
+        w[-1] = n_req - (n_units - 1) * bs
+    else:
+        blk = blocks_for_len(lengths).astype(np.float64)
+        pad = n_units * bs - n_req
+        if pad:
+            blk = np.concatenate([blk, np.zeros(pad)])
+        w = blk.reshape(n_units, bs).sum(axis=1)
+    cum = np.cumsum(w)
+    total = cum[-1]
+    cuts = [0]
+    for r in range(1, world):
+        u = int(np.searchsorted(cum, total * r / world, side="left")) + 1
+        u = min(max(u, cuts[-1]), n_units)
+        cuts.append(u)
+    cuts.append(n_units)
+    return [(min(a * bs, n_req), min(b * bs, n_req)) for a, b in zip(cuts[:-1], cuts[1:])]
+
+
+def batch_lists(n_req: int, batch_size: int, first_req: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """(idx, batch_first) for consecutive BatchSize groups of request digests,
+    in origin order (the last batch may be short).  idx is relative to first_req."""
+    n_b = (n_req + batch_size - 1) // batch_size
+    idx = np.arange(n_req, dtype=np.uint32)
+    first = np.minimum(np.arange(n_b + 1, dtype=np.int64) * batch_size, n_req).astype(np.uint32)
+    return idx, first

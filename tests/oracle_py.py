@@ -1,0 +1,97 @@
+"""ctypes wrapper of the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+NULL = 0xFFFFFFFF
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def load() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    src = os.path.join(ORACLE_DIR, "sha256_oracle.c")
+    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+        build()
+    lib = ctypes.CDLL(ORACLE_SO)
+    vp = ctypes.c_void_p
+    lib.oracle_hash_requests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
+    lib.oracle_hash_requests_mt.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int]
+    lib.oracle_batch_digests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
+    lib.oracle_gen_requests.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, vp]
+    lib.oracle_sha256_force_impl.argtypes = [ctypes.c_int]
+    lib.oracle_sha256_has_shani.restype = ctypes.c_int
+    lib.oracle_splitmix64.argtypes = [ctypes.c_uint64]
+    lib.oracle_splitmix64.restype = ctypes.c_uint64
+    _lib = lib
+    return lib
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data if a.size else None
+
+
+def hash_requests(arena, off, length, threads: int = 1) -> np.ndarray:
+    lib = load()
+    a = np.ascontiguousarray(np.frombuffer(memoryview(arena), dtype=np.uint8) if not isinstance(arena, np.ndarray)
+                             else arena.reshape(-1).view(np.uint8))
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(length, dtype=np.uint32)
+    out = np.empty((o.size, 32), dtype=np.uint8)
+    if o.size:
+        if threads > 1:
+            lib.oracle_hash_requests_mt(_p(a), _p(o), _p(ln), o.size, _p(out), threads)
+        else:
+            lib.oracle_hash_requests(_p(a), _p(o), _p(ln), o.size, _p(out))
+    return out
+
+
+def hash_messages(messages) -> np.ndarray:
+    lens = np.array([len(m) for m in messages], dtype=np.uint32)
+    off = np.zeros(len(messages), dtype=np.uint64)
+    if len(messages) > 1:
+        np.cumsum(lens[:-1], out=off[1:])
+    return hash_requests(b"".join(messages) or b"\0", off, lens)
+
+
+def batch_digests(req_digests: np.ndarray, idx, first) -> np.ndarray:
+    lib = load()
+    d = np.ascontiguousarray(req_digests, dtype=np.uint8).reshape(-1, 32)
+    ix = np.ascontiguousarray(idx, dtype=np.uint32)
+    fs = np.ascontiguousarray(first, dtype=np.uint32)
+    nb = fs.size - 1
+    out = np.empty((nb, 32), dtype=np.uint8)
+    if nb:
+        lib.oracle_batch_digests(_p(d), _p(ix), _p(fs), nb, _p(out))
+    return out
+
+
+def gen_requests(seed: int, first: int, count: int, data_len: int) -> np.ndarray:
+    lib = load()
+    out = np.empty(count * (16 + data_len), dtype=np.uint8)
+    lib.oracle_gen_requests(seed, first, count, data_len, _p(out))
+    return out
+
+
+def force_impl(impl: int) -> None:
+    load().oracle_sha256_force_impl(impl)
+
+
+def has_shani() -> bool:
+    return bool(load().oracle_sha256_has_shani())

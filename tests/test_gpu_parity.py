@@ -1,0 +1,351 @@
+"""Parity of the gfx950 HIP path (through the C-ABI) with the CPU oracle and the
+golden fixtures.  Bit-exact: SHA-256 is integer/byte work.
+
+Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+import oracle_py
+import synth
+from mirbft_amd import (ActionResults, Actions, Engine, HashRequest, MirshaError, Processor, ProcessorWorkPool,
+                        gpu_hasher, hash_batch_multi, hashdata, sharding)
+from mirbft_amd import _lib
+from mirbft_amd.engine import KERNEL_LISTS, KERNEL_MSGS, VARIANT_DIRECT, VARIANT_LDS
+
+pytestmark = pytest.mark.gpu
+
+EMPTY = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
+
+
+@pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT], ids=["lds", "direct"])
+def eng(engine, request):
+    engine.set_variant(request.param)
+    yield engine
+    engine.set_variant(VARIANT_LDS)
+
+
+def _hex(rows):
+    return [r.tobytes().hex() for r in rows]
+
+
+def test_nist_vectors(eng, kat):
+    got = eng.hash_messages([v["ascii"].encode() for v in kat["nist"]] + [b"a" * 1_000_000])
+    assert _hex(got) == [v["sha256"] for v in kat["nist"]] + [kat["million_a"]]
+
+
+def test_boundary_lengths(eng, kat):
+    vs = kat["boundary"]
+    got = eng.hash_messages([synth.pattern_bytes(v["len"], v["salt"]) for v in vs])
+    assert _hex(got) == [v["sha256"] for v in vs]
+
+
+def test_empty_message_and_empty_call(eng):
+    assert _hex(eng.hash_messages([b""])) == [EMPTY]
+    assert eng.hash_messages([]).shape == (0, 32)
+    assert eng.hash_batch(b"", [], []).shape == (0, 32)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_lengths_misaligned_offsets(eng, seed):
+    """Any byte alignment, gaps between messages, overlapping messages."""
+    rng = np.random.default_rng(seed)
+    n = 3000
+    lens = rng.integers(0, 2100, n).astype(np.uint32)
+    gaps = rng.integers(0, 9, n).astype(np.uint64)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])
+    off[::17] = off[::17] // 3  # some overlapping / out-of-order messages
+    arena = rng.integers(0, 256, int((off + lens).max()) + 5, dtype=np.uint8)
+    got = eng.hash_batch(arena, off, lens)
+    want = oracle_py.hash_requests(arena, off, lens)
+    assert np.array_equal(got, want)
+
+
+def test_every_length_0_to_600_every_alignment(eng):
+    msgs = []
+    for L in range(0, 601):
+        msgs.append(bytes(((j * 29 + L) & 0xFF) for j in range(L)))
+    # pack with a rotating 0..3 byte shift so every (length, alignment) pair occurs
+    off, arena, pos = [], bytearray(), 0
+    for i, m in enumerate(msgs):
+        pad = (i * 5) % 4
+        arena += b"\xAA" * pad
+        pos += pad
+        off.append(pos)
+        arena += m
+        pos += len(m)
+    lens = [len(m) for m in msgs]
+    got = eng.hash_batch(bytes(arena), off, lens)
+    assert _hex(got) == [hashlib.sha256(m).hexdigest() for m in msgs]
+
+
+def test_mixed_buckets_origin_order(eng):
+    """Lengths spanning 1..1000 blocks go through the bucketing permutation;
+    digests must still come back at their origin index."""
+    lens = synth.log_uniform_lengths(synth.SEED_BASE + 5, 700, 0, 16)
+    msgs = [synth.data_bytes(99, i, int(n)) for i, n in enumerate(lens)]
+    got = eng.hash_messages(msgs)
+    assert np.array_equal(got, oracle_py.hash_messages(msgs))
+
+
+def test_loguniform_fixture(eng, synth_fx):
+    fx = synth_fx["loguniform"]
+    msgs = [synth.data_bytes(fx["seed"], i, n) for i, n in enumerate(fx["lengths"])]
+    assert _hex(eng.hash_messages(msgs)) == fx["sha256"]
+
+
+def test_large_single_message(eng):
+    rng = np.random.default_rng(11)
+    m = rng.integers(0, 256, (16 << 20) + 13, dtype=np.uint8).tobytes()
+    assert eng.hash_messages([m])[0].tobytes() == hashlib.sha256(m).digest()
+
+
+def test_testengine_requests(eng, layouts):
+    rs = layouts["testengine_requests"]
+    reqs = [hashdata.request_hash_data(r["client"], r["req_no"],
+                                       hashdata.testengine_request_payload(r["client"], r["req_no"])) for r in rs]
+    got = eng.hash_slices(reqs)
+    assert _hex(got) == [r["sha256"] for r in rs]
+
+
+def _digest_table(layouts):
+    keys = {(r["client"], r["req_no"]): i for i, r in enumerate(layouts["testengine_requests"])}
+    dig = np.frombuffer(b"".join(bytes.fromhex(r["sha256"]) for r in layouts["testengine_requests"]),
+                        dtype=np.uint8).reshape(-1, 32)
+    return keys, dig
+
+
+def test_batches_with_null_requests(engine, layouts):
+    keys, dig = _digest_table(layouts)
+    idx, first = [], [0]
+    for b in layouts["batches"]:
+        idx += [_lib.MIRSHA_NULL_INDEX if e is None else keys[(e[0], e[1])] for e in b["entries"]]
+        first.append(len(idx))
+    got = engine.digest_lists(dig, idx, first)
+    assert _hex(got) == [b["sha256"] for b in layouts["batches"]]
+
+
+def test_batch_slices_equal_digest_lists(engine, layouts):
+    """The same batches fed as [][]byte HashRequest.Data (sequence.go:154-157)."""
+    keys, dig = _digest_table(layouts)
+    reqs = []
+    for b in layouts["batches"]:
+        reqs.append(hashdata.batch_hash_data([b"" if e is None else dig[keys[(e[0], e[1])]].tobytes()
+                                              for e in b["entries"]]))
+    assert _hex(engine.hash_slices(reqs)) == [b["sha256"] for b in layouts["batches"]]
+
+
+def test_checkpoint_chain(engine, layouts):
+    keys, dig = _digest_table(layouts)
+    cc = layouts["checkpoint_chain"]
+    commits = [keys[(c, r)] for c, r in cc["commits"]]
+    idx, first, want, start = [], [0], [], 0
+    for cp in cc["checkpoints"]:
+        idx += commits[start:cp["after_commit"]]
+        first.append(len(idx))
+        want.append(cp.get("sha256") or cp.get("empty_after_reset"))
+        start = cp["after_commit"]
+    assert _hex(engine.digest_lists(dig, idx, first)) == want
+    assert want[-1] == EMPTY  # testengine/recorder_test.go:83
+
+
+def test_epoch_change(engine, layouts):
+    ec = layouts["epoch_change"]
+    slices = hashdata.epoch_change_hash_data(
+        ec["new_epoch"], [(s, bytes.fromhex(v)) for s, v in ec["checkpoints"]],
+        [(e, s, bytes.fromhex(d)) for e, s, d in ec["p_set"]], [(e, s, bytes.fromhex(d)) for e, s, d in ec["q_set"]])
+    assert _hex(engine.hash_slices([slices] * 3)) == [ec["sha256"]] * 3
+
+
+def test_slices_with_empty_slices_and_requests(engine):
+    reqs = [[], [b""], [b"", b"", b"abc"], [b"ab", b"", b"c"], [b"x" * 63, b"y"], [b"q" * 1000] * 5]
+    want = [hashlib.sha256(b"".join(r)).hexdigest() for r in reqs]
+    assert _hex(engine.hash_slices(reqs)) == want
+
+
+def test_cfg2_prefix_requests_then_batches(eng, synth_fx):
+    fx = synth_fx["cfg2_prefix"]
+    n, bs = fx["count"], fx["batch_size"]
+    arena = synth.request_arena(synth.SEED_BASE + 2, 0, n, 256)
+    idx, first = sharding.batch_lists(n, bs)
+    req, bat = eng.hash_requests_then_batches(arena, np.arange(n) * 272, np.full(n, 272), idx, first)
+    assert hashlib.sha256(req.tobytes()).hexdigest() == fx["request_sha256_of_concat"]
+    assert _hex(bat) == fx["batch_sha256"]
+
+
+def test_requests_then_batches_random_with_nulls(eng):
+    rng = np.random.default_rng(5)
+    n = 5000
+    lens = rng.integers(0, 700, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(lens[:-1], out=off[1:])
+    arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    sizes = rng.integers(0, 40, 400)
+    idx = rng.integers(0, n, int(sizes.sum())).astype(np.uint32)
+    idx[rng.random(idx.size) < 0.1] = _lib.MIRSHA_NULL_INDEX
+    first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    req, bat = eng.hash_requests_then_batches(arena, off, lens, idx, first)
+    want_req = oracle_py.hash_requests(arena, off, lens)
+    assert np.array_equal(req, want_req)
+    assert np.array_equal(bat, oracle_py.batch_digests(want_req, idx, first))
+
+
+def test_invalid_arguments_raise(engine):
+    with pytest.raises(MirshaError):
+        engine.hash_batch(b"abc", [2], [5])  # past the arena end
+    with pytest.raises(MirshaError):
+        engine.digest_lists(np.zeros((2, 32), np.uint8), [0, 5], [0, 2])  # idx out of range
+    with pytest.raises(MirshaError):
+        engine.digest_lists(np.zeros((2, 32), np.uint8), [0, 1], [1, 2])  # first[0] != 0
+    # the context is still usable afterwards
+    assert _hex(engine.hash_messages([b""])) == [EMPTY]
+
+
+def test_processor_mirror_origin_order(engine):
+    reqs = [HashRequest(data=hashdata.request_hash_data(c, r, b"payload-%d" % (c * 7 + r)), origin=("req", c, r))
+            for c in range(3) for r in range(50)]
+    reqs += [HashRequest(data=hashdata.batch_hash_data([b"\x01" * 32] * k), origin=("batch", k)) for k in (1, 20, 0)]
+    res = Processor(engine).process(Actions(hash=reqs))
+    assert isinstance(res, ActionResults) and len(res.digests) == len(reqs)
+    for hr, req in zip(res.digests, reqs):
+        assert hr.request is req
+        assert hr.digest == hashlib.sha256(hashdata.concat(req.data)).digest()
+    pool = ProcessorWorkPool(engine, hash_workers=8)
+    res2 = pool.process(Actions(hash=reqs))
+    assert [r.digest for r in res2.digests] == [r.digest for r in res.digests]
+    assert Processor(engine).process(Actions()).digests == []
+
+
+def test_streaming_hasher(engine):
+    h = gpu_hasher(engine)()
+    for part in (b"ab", b"", b"c"):
+        h.write(part)
+    assert h.sum().hex() == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"
+    h.reset()
+    assert h.sum().hex() == EMPTY
+
+
+def test_cpp_host_mirror():
+    host = ctypes.CDLL(_lib.HOST_LIB_PATH)
+    msgs = [b"", b"abc", b"z" * 1000]
+    bufs = [ctypes.create_string_buffer(m, len(m) or 1) for m in msgs]
+    ptrs = (ctypes.c_void_p * 3)(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_uint64 * 3)(*[len(m) for m in msgs])
+    out = (ctypes.c_uint8 * 96)()
+    err = ctypes.create_string_buffer(256)
+    rc = host.mirbft_host_process(0, ptrs, lens, 3, out, err, 256)
+    assert rc == 0, err.value
+    assert [bytes(out[32 * i:32 * i + 32]) for i in range(3)] == [hashlib.sha256(m).digest() for m in msgs]
+
+
+def test_multi_device_sharding_in_process(engine):
+    """mirsha_hash_batch_multi on [0, 0]: two contexts, contiguous ranges, host gather."""
+    rng = np.random.default_rng(3)
+    n = 4001
+    lens = rng.integers(0, 900, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(lens[:-1], out=off[1:])
+    arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    got = hash_batch_multi([0, 0], arena, off, lens)
+    assert np.array_equal(got, oracle_py.hash_requests(arena, off, lens))
+
+
+# ---------------------------------------------------------------- device API
+
+
+def _torch():
+    import torch
+
+    assert torch.cuda.is_available()
+    return torch
+
+
+def test_device_generator_matches_oracle(engine):
+    torch = _torch()
+    for data_len, first, count in ((256, 0, 300), (4096, 1 << 17, 40), (17, 5, 9), (0, 3, 4)):
+        d = torch.empty(count * (16 + data_len), dtype=torch.uint8, device="cuda")
+        engine.synth_requests_device(synth.SEED_BASE + 2, first, count, data_len, d.data_ptr())
+        engine.sync()
+        want = oracle_py.gen_requests(synth.SEED_BASE + 2, first, count, data_len)
+        assert np.array_equal(d.cpu().numpy(), want), (data_len, first)
+
+
+@pytest.mark.parametrize("cfg,data_len,n,bs", [(2, 256, 1 << 20, 20), (3, 4096, 1 << 18, 500)])
+def test_full_size_configs_device_resident(engine, cfg, data_len, n, bs):
+    """BASELINE configs 2 and 3 at full size, device-resident, bit-exact vs the
+    oracle (multi-threaded CPU), plus the dependent batch pass."""
+    torch = _torch()
+    stride = 16 + data_len
+    seed = synth.SEED_BASE + cfg
+    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    d_req = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    idx, first = sharding.batch_lists(n, bs)
+    d_idx = torch.from_numpy(idx.astype(np.int32)).cuda()
+    d_first = torch.from_numpy(first.astype(np.int32)).cuda()
+    nb = first.size - 1
+    d_bat = torch.empty((nb, 32), dtype=torch.uint8, device="cuda")
+    engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
+    engine.hash_batch_device(d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr(), None, n,
+                             d_req.data_ptr())
+    engine.digest_lists_device(d_req.data_ptr(), d_idx.data_ptr(), d_first.data_ptr(), nb, d_bat.data_ptr())
+    engine.sync()
+    arena = oracle_py.gen_requests(seed, 0, n, data_len)
+    want_req = oracle_py.hash_requests(arena, np.arange(n, dtype=np.uint64) * stride, np.full(n, stride), threads=8)
+    got_req = d_req.cpu().numpy()
+    assert np.array_equal(got_req, want_req)
+    assert np.array_equal(d_bat.cpu().numpy(), oracle_py.batch_digests(want_req, idx, first))
+
+
+def test_external_stream_and_timing(engine):
+    torch = _torch()
+    s = torch.cuda.Stream()
+    n, data_len = 4096, 256
+    d_arena = torch.empty(n * 272, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * 272
+    d_len = torch.full((n,), 272, dtype=torch.int32, device="cuda")
+    d_out = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    engine.set_stream(s.cuda_stream)
+    engine.set_timing(True)
+    engine.reset_timing()
+    try:
+        engine.synth_requests_device(7, 0, n, data_len, d_arena.data_ptr())
+        for _ in range(3):
+            engine.hash_batch_device(d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr(), None, n,
+                                     d_out.data_ptr())
+        s.synchronize()
+        launches, ms = engine.kernel_time(KERNEL_MSGS)
+        assert launches == 3 and ms > 0
+        assert engine.kernel_time(KERNEL_LISTS)[0] == 0
+    finally:
+        engine.set_timing(False)
+        engine.set_stream(None)
+    want = oracle_py.hash_requests(oracle_py.gen_requests(7, 0, n, data_len), np.arange(n) * 272, np.full(n, 272))
+    assert np.array_equal(d_out.cpu().numpy(), want)
+
+
+def test_device_order_permutation(engine):
+    torch = _torch()
+    rng = np.random.default_rng(8)
+    n = 3000
+    lens = rng.integers(0, 3000, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(lens[:-1], out=off[1:])
+    arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    from mirbft_amd import bucket_order
+
+    order, _ = bucket_order(lens)
+    d_arena = torch.from_numpy(arena).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+    d_order = torch.from_numpy(order.view(np.int32)).cuda()
+    d_out = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    engine.hash_batch_device(d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(), d_order.data_ptr(), n,
+                             d_out.data_ptr())
+    engine.sync()
+    assert np.array_equal(d_out.cpu().numpy(), oracle_py.hash_requests(arena, off, lens))
