@@ -32,21 +32,33 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // 16-byte chunk q of block blk of a message at arena offset o, length L,
 // as 4 big-endian SHA words with padding applied.
-__device__ __forceinline__ void load_chunk(__amdgpu_buffer_rsrc_t rsrc, uint32_t o, uint32_t L,
+__device__ __forceinline__ void load_chunk(__amdgpu_buffer_rsrc_t rsrc, uint32_t records, uint32_t o, uint32_t L,
                                            uint32_t blk, uint32_t q, bool last_block,
                                            uint32_t out[4]) {
     const uint32_t p = 64u * blk + 16u * q;
     const uint32_t addr = o + p;
     const uint32_t a = addr & ~3u;
     const uint32_t sel = be_sel(addr & 3u);
-    // Raw buffer loads: range-checked against the arena length, so reads past
-    // the arena end return 0 instead of faulting.
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a, 0, 0);
-    const uint32_t v4 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
-    out[0] = be_word(v[1], v[0], sel);
-    out[1] = be_word(v[2], v[1], sel);
-    out[2] = be_word(v[3], v[2], sel);
-    out[3] = be_word(v4, v[3], sel);
+    // Raw buffer loads are range-checked against num_records (the arena length
+    // rounded up to 4): past the end they return 0 instead of faulting.  The
+    // check covers a whole access, so a 16-byte load that straddles the end
+    // would lose its in-range bytes: the arena's last chunk takes 5 dword loads.
+    uint32_t v0, v1, v2, v3, v4;
+    if (a + 20u <= records) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a, 0, 0);
+        v0 = v[0]; v1 = v[1]; v2 = v[2]; v3 = v[3];
+        v4 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
+    } else {
+        v0 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a, 0, 0);
+        v1 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 4u, 0, 0);
+        v2 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 8u, 0, 0);
+        v3 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 12u, 0, 0);
+        v4 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
+    }
+    out[0] = be_word(v1, v0, sel);
+    out[1] = be_word(v2, v1, sel);
+    out[2] = be_word(v3, v2, sel);
+    out[3] = be_word(v4, v3, sel);
     if (p + 16u > L) pad_chunk(out, p, L, last_block, q);
 }
 
@@ -83,8 +95,11 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     const uint32_t nb = valid ? blocks_for_len(L) : 0u;
     const uint32_t wave_nb = wave_max(nb);
 
+    // Bytes past arena_len inside the last dword are never part of a message
+    // (they are masked by the padding logic), so the range rounds up to 4.
+    const uint32_t records = (arena_len + 3u) & ~3u;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)arena_len, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)records, 0x00020000);
 
     uint32_t st[8];
 #pragma unroll
@@ -107,7 +122,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
             for (int j = 0; j < 4; j++) {
                 if (blk < nbj[j]) {
                     uint32_t wq[4];
-                    load_chunk(rsrc, oj[j], Lj[j], blk, q, blk + 1u == nbj[j], wq);
+                    load_chunk(rsrc, records, oj[j], Lj[j], blk, q, blk + 1u == nbj[j], wq);
                     my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
                 }
             }
@@ -133,7 +148,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
                 uint32_t w[16];
                 const bool last = blk + 1u == nb;
 #pragma unroll
-                for (int q = 0; q < 4; q++) load_chunk(rsrc, o, L, blk, (uint32_t)q, last, &w[4 * q]);
+                for (int q = 0; q < 4; q++) load_chunk(rsrc, records, o, L, blk, (uint32_t)q, last, &w[4 * q]);
                 compress(st, w);
             }
         }
