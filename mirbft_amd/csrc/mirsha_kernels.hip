@@ -30,36 +30,65 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     return v;
 }
 
-// 16-byte chunk q of block blk of a message at arena offset o, length L,
-// as 4 big-endian SHA words with padding applied.
-__device__ __forceinline__ void load_chunk(__amdgpu_buffer_rsrc_t rsrc, uint32_t records, uint32_t o, uint32_t L,
-                                           uint32_t blk, uint32_t q, bool last_block,
-                                           uint32_t out[4]) {
-    const uint32_t p = 64u * blk + 16u * q;
-    const uint32_t addr = o + p;
-    const uint32_t a = addr & ~3u;
-    const uint32_t sel = be_sel(addr & 3u);
-    // Raw buffer loads are range-checked against num_records (the arena length
-    // rounded up to 4): past the end they return 0 instead of faulting.  The
-    // check covers a whole access, so a 16-byte load that straddles the end
-    // would lose its in-range bytes: the arena's last chunk takes 5 dword loads.
-    uint32_t v0, v1, v2, v3, v4;
-    if (a + 20u <= records) {
+// Raw 20 bytes (5 dwords) covering the 16-byte chunk q of block blk of a
+// message at arena offset o: aligned down to 4 bytes, the byte shift is
+// resolved later by v_perm.  Inactive chunks read at an out-of-range offset,
+// which the buffer range check turns into zeros without a memory access.
+struct RawChunk {
+    uint32_t v[5];
+    uint32_t sel;
+};
+
+__device__ __forceinline__ void issue_chunk(__amdgpu_buffer_rsrc_t rsrc, uint32_t records, uint32_t o,
+                                            uint32_t blk, uint32_t q, bool active, RawChunk& c) {
+    const uint32_t addr = o + 64u * blk + 16u * q;
+    const uint32_t a = active ? (addr & ~3u) : 0xFFFFFFE0u;
+    c.sel = be_sel(addr & 3u);
+    // The range check covers a whole access: a 16-byte load straddling the end
+    // of the arena would return 0 for its in-range bytes too.  The arena's last
+    // chunk therefore takes 5 dword loads — in asm, because hipcc otherwise
+    // merges adjacent buffer dword loads back into one dwordx4.
+    if (a + 20u <= records || !active) {
         const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a, 0, 0);
-        v0 = v[0]; v1 = v[1]; v2 = v[2]; v3 = v[3];
-        v4 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
+        c.v[0] = v[0]; c.v[1] = v[1]; c.v[2] = v[2]; c.v[3] = v[3];
+        c.v[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
     } else {
-        v0 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a, 0, 0);
-        v1 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 4u, 0, 0);
-        v2 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 8u, 0, 0);
-        v3 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 12u, 0, 0);
-        v4 = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
+        asm volatile(
+            "s_nop 4\n\t"
+            "buffer_load_dword %0, %5, %6, 0 offen\n\t"
+            "buffer_load_dword %1, %5, %6, 0 offen offset:4\n\t"
+            "buffer_load_dword %2, %5, %6, 0 offen offset:8\n\t"
+            "buffer_load_dword %3, %5, %6, 0 offen offset:12\n\t"
+            "buffer_load_dword %4, %5, %6, 0 offen offset:16\n\t"
+            "s_waitcnt vmcnt(0)"
+            : "=&v"(c.v[0]), "=&v"(c.v[1]), "=&v"(c.v[2]), "=&v"(c.v[3]), "=&v"(c.v[4])
+            : "v"(a), "s"(rsrc)
+            : "memory");
     }
-    out[0] = be_word(v1, v0, sel);
-    out[1] = be_word(v2, v1, sel);
-    out[2] = be_word(v3, v2, sel);
-    out[3] = be_word(v4, v3, sel);
-    if (p + 16u > L) pad_chunk(out, p, L, last_block, q);
+}
+
+// Big-endian SHA words of the chunk at message byte position p, with FIPS
+// 180-4 §5.1.1 padding (0x80, zeros, 64-bit bit length in words 14/15 of the
+// last block) applied branch-free on chunks that reach past the message end.
+__device__ __forceinline__ void finish_chunk(const RawChunk& c, uint32_t p, uint32_t L, bool last_block,
+                                             uint32_t q, uint32_t out[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) out[k] = be_word(c.v[k + 1], c.v[k], c.sel);
+    if (p + 16u > L) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int32_t t = (int32_t)(L - (p + 4u * k));  // message bytes left at this word
+            const uint32_t sh = (uint32_t)t << 3;          // only used when 0 <= t <= 3
+            const uint32_t keep = ~(0xFFFFFFFFu >> sh);    // the t leading data bytes
+            const uint32_t mark = 0x80000000u >> sh;       // the 0x80 byte right after them
+            const uint32_t part = (out[k] & keep) | mark;
+            out[k] = t >= 4 ? out[k] : (t < 0 ? 0u : part);
+        }
+        if (last_block && q == 3u) {
+            out[2] = L >> 29;
+            out[3] = L << 3;
+        }
+    }
 }
 
 // Swizzled 16-byte slot of (message m, quarter q) inside a wave's 256-slot tile.
@@ -118,16 +147,18 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
         }
         uint4* my = tile[wv];
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
+            RawChunk rc[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) issue_chunk(rsrc, records, oj[j], blk, q, blk < nbj[j], rc[j]);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (blk < nbj[j]) {
-                    uint32_t wq[4];
-                    load_chunk(rsrc, records, oj[j], Lj[j], blk, q, blk + 1u == nbj[j], wq);
-                    my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
-                }
+                uint32_t wq[4];
+                finish_chunk(rc[j], 64u * blk + 16u * q, Lj[j], blk + 1u == nbj[j], q, wq);
+                // Unconditional: a slot of a finished message is never read.
+                my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
             }
             // Cross-lane hand-off inside one wave: LDS ops of a wave execute in
-            // order; the fence only stops the compiler from reordering them.
+            // order; the fences only stop the compiler from reordering them.
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -144,13 +175,15 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
         }
     } else {
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
-            if (blk < nb) {
-                uint32_t w[16];
-                const bool last = blk + 1u == nb;
+            const bool active = blk < nb;
+            RawChunk rc[4];
 #pragma unroll
-                for (int q = 0; q < 4; q++) load_chunk(rsrc, records, o, L, blk, (uint32_t)q, last, &w[4 * q]);
-                compress(st, w);
-            }
+            for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, blk, (uint32_t)q, active, rc[q]);
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
+            if (active) compress(st, w);
         }
     }
     if (valid) store_digest(out, msg, st);
