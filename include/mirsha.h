@@ -71,8 +71,10 @@ const char* mirsha_last_error(const mirsha_ctx* ctx);
 int mirsha_ctx_set_stream(mirsha_ctx* ctx, void* hip_stream);
 void* mirsha_ctx_stream(mirsha_ctx* ctx);
 
-/* Kernel variant for sha256 over packed messages: 0 = LDS-staged coalesced
- * loader (default), 1 = direct per-lane loads.  For A/B measurement. */
+/* Kernel variant for sha256 over packed messages (A/B measurement):
+ * 0 = LDS-staged coalesced loader + generated-asm rounds (default),
+ * 1 = direct per-lane loads + asm rounds, 2 = LDS loader + compiler-scheduled
+ * C++ rounds, 3 = direct loads + C++ rounds.  All are bit-exact. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
 /* Per-kernel device-time accounting with HIP events on the launch stream.

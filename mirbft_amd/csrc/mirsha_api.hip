@@ -349,7 +349,7 @@ int mirsha_ctx_set_stream(mirsha_ctx* c, void* s) {
 void* mirsha_ctx_stream(mirsha_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
 
 int mirsha_ctx_set_variant(mirsha_ctx* c, int v) {
-    if (!c || (v != mirsha::kVariantLds && v != mirsha::kVariantDirect)) return MIRSHA_EINVAL;
+    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantDirectCxx) return MIRSHA_EINVAL;
     c->variant = v;
     return MIRSHA_OK;
 }

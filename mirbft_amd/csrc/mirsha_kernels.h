@@ -9,7 +9,9 @@ constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kBlockThreads = 64 * kWavesPerBlock;
 constexpr uint32_t kNullIndex = 0xFFFFFFFFu;
 
-enum : int { kVariantLds = 0, kVariantDirect = 1 };
+// sha256_msgs_kernel variants: loader (LDS-staged / direct per-lane loads) x
+// rounds (generated asm / compiler-scheduled C++).  Default: kVariantLds.
+enum : int { kVariantLds = 0, kVariantDirect = 1, kVariantLdsCxx = 2, kVariantDirectCxx = 3 };
 
 hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t* off,
                        const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,

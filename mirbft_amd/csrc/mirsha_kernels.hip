@@ -104,7 +104,15 @@ __device__ __forceinline__ void store_digest(uint8_t* out, uint32_t msg, const u
                       __builtin_bswap32(st[7]));
 }
 
-template <bool kLds>
+template <bool kAsm>
+__device__ __forceinline__ void compress_v(uint32_t st[8], uint32_t w[16]) {
+    if constexpr (kAsm)
+        compress_asm(st, w);
+    else
+        compress(st, w);
+}
+
+template <bool kLds, bool kAsm>
 __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     const uint8_t* __restrict__ arena, uint32_t arena_len, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (blk < nb) compress(st, w);
+            if (blk < nb) compress_v<kAsm>(st, w);
         }
     } else {
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
@@ -183,7 +191,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
-            if (active) compress(st, w);
+            if (active) compress_v<kAsm>(st, w);
         }
     }
     if (valid) store_digest(out, msg, st);
@@ -233,7 +241,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
                 w[14] = L >> 29;
                 w[15] = L << 3;
             }
-            compress(st, w);
+            compress_asm(st, w);
         }
     }
     if (valid) store_digest(out, k, st);
@@ -277,10 +285,20 @@ hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t*
     if (n == 0) return hipSuccess;
     const uint32_t tiles = (n + 63u) / 64u;
     const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
-    if (variant == kVariantDirect)
-        sha256_msgs_kernel<false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
-    else
-        sha256_msgs_kernel<true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+    switch (variant) {
+        case kVariantLds:
+            sha256_msgs_kernel<true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+            break;
+        case kVariantDirect:
+            sha256_msgs_kernel<false, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+            break;
+        case kVariantLdsCxx:
+            sha256_msgs_kernel<true, false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+            break;
+        default:
+            sha256_msgs_kernel<false, false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+            break;
+    }
     return hipGetLastError();
 }
 

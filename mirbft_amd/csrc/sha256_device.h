@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sha256_rounds_asm.h"
+
 namespace mirsha {
 
 static constexpr uint32_t kK[64] = {
@@ -67,6 +69,18 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
 #undef MIRSHA_ROUND
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// The same compression with the 64 rounds in generated gfx950 assembly
+// (sha256_rounds_asm.h): a..h + W[16] + 4 temporaries, no compiler-hoisted
+// schedule partial sums.
+__device__ __forceinline__ void compress_asm(uint32_t st[8], uint32_t w[16]) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = st[i];
+    rounds_asm(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] += s[i];
 }
 
 // Number of 64-byte compressions for an L-byte message: ceil((L + 9) / 64).

@@ -20,6 +20,8 @@ KERNEL_LISTS = 1
 KERNEL_GEN = 2
 VARIANT_LDS = 0
 VARIANT_DIRECT = 1
+VARIANT_LDS_CXX = 2
+VARIANT_DIRECT_CXX = 3
 
 
 def _ptr(a: np.ndarray | None) -> int | None:
