@@ -153,7 +153,8 @@ def main():
     def step():
         eng.hash_batch_device(d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr(), None, n,
                               d_req.data_ptr())
-        eng.digest_lists_device(d_req.data_ptr(), d_idx.data_ptr(), d_first.data_ptr(), nbat, d_bat.data_ptr())
+        eng.digest_lists_device(d_req.data_ptr(), n, d_idx.data_ptr(), d_first.data_ptr(), nbat, int(first[-1]),
+                                d_bat.data_ptr())
 
     for _ in range(a.warmup):
         step()

@@ -133,9 +133,13 @@ int mirsha_hash_batch_device(mirsha_ctx* ctx, const uint8_t* d_arena, uint64_t a
                              const uint64_t* d_off, const uint32_t* d_len,
                              const uint32_t* d_order, uint32_t n, uint8_t* d_digests_out);
 
-int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, const uint32_t* d_idx,
-                               const uint32_t* d_list_first, uint32_t n_lists,
-                               uint8_t* d_digests_out);
+/* d_digests holds n_digests 32-byte digests (< 2^27; reads are range-checked,
+ * an out-of-range index reads zeros).  n_entries = d_list_first[n_lists] (the
+ * caller knows it; it sizes the library's scratch for lists that contain
+ * MIRSHA_NULL_INDEX entries). */
+int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, uint32_t n_digests,
+                               const uint32_t* d_idx, const uint32_t* d_list_first, uint32_t n_lists,
+                               uint32_t n_entries, uint8_t* d_digests_out);
 
 /* Host helper: order[] = message indices sorted by SHA-256 block count,
  * longest first (stable), so a wave's 64 lanes run equal-length chains.

@@ -58,7 +58,10 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p],
     ),
-    "mirsha_digest_lists_device": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
+    "mirsha_digest_lists_device": (
+        c_int,
+        [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint32, c_uint32, c_void_p],
+    ),
     "mirsha_bucket_order": (c_int, [c_void_p, c_uint32, c_void_p]),
     "mirsha_hash_batch_multi": (
         c_int,

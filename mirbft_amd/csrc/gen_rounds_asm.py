@@ -45,7 +45,7 @@ def op(i):
     return f"%{i}"
 
 
-def block(j0):
+def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr"):
     lines = []
     for r in range(8):
         j = j0 + r
@@ -63,32 +63,148 @@ def block(j0):
                 f"v_alignbit_b32 {t2}, {w2}, {w2}, 19",
                 f"v_lshrrev_b32_e32 {t3}, 10, {w2}",
                 f"v_bitop3_b32 {t1}, {t1}, {t2}, {t3} bitop3:0x96",
-                f"v_add3_u32 {wj}, {wj}, {t0}, {t1}",
-                f"v_add_u32_e32 {wj}, {wj}, {w7}",
             ]
+            if add_mode == "add3":
+                lines += [f"v_add3_u32 {wj}, {wj}, {t0}, {t1}", f"v_add_u32_e32 {wj}, {wj}, {w7}"]
+            else:
+                lines += [f"v_add_u32_e32 {wj}, {wj}, {t0}", f"v_add_u32_e32 {wj}, {wj}, {t1}",
+                          f"v_add_u32_e32 {wj}, {wj}, {w7}"]
         lines += [
             f"v_alignbit_b32 {t0}, {e}, {e}, 6",
             f"v_alignbit_b32 {t1}, {e}, {e}, 11",
             f"v_alignbit_b32 {t2}, {e}, {e}, 25",
             f"v_bitop3_b32 {t0}, {t0}, {t1}, {t2} bitop3:0x96",
-            f"v_bfi_b32 {t1}, {e}, {f}, {g}",
-            f"v_add3_u32 {h}, {h}, {t0}, {t1}",
-            f"v_add3_u32 {h}, {h}, {op(KOP[r])}, {wj}",
+        ]
+        if ch_mode == "bfi":
+            lines.append(f"v_bfi_b32 {t1}, {e}, {f}, {g}")
+        else:  # Ch(e,f,g) = e ? f : g, truth table 0xCA with src0=0xF0, src1=0xCC, src2=0xAA
+            lines.append(f"v_bitop3_b32 {t1}, {e}, {f}, {g} bitop3:0xca")
+        if add_mode == "add3":
+            lines.append(f"v_add3_u32 {h}, {h}, {t0}, {t1}")
+        else:
+            lines += [f"v_add_u32_e32 {h}, {h}, {t0}", f"v_add_u32_e32 {h}, {h}, {t1}"]
+        if k_mode == "sgpr":
+            lines.append(f"v_add3_u32 {h}, {h}, {op(KOP[r])}, {wj}")
+        else:  # VOP2 with a 32-bit literal: h += K, h += W
+            lines += [f"v_add_u32_e32 {h}, 0x{K[j]:08x}, {h}", f"v_add_u32_e32 {h}, {h}, {wj}"]
+        lines += [
             f"v_add_u32_e32 {d}, {d}, {h}",
             f"v_alignbit_b32 {t0}, {a}, {a}, 2",
             f"v_alignbit_b32 {t1}, {a}, {a}, 13",
             f"v_alignbit_b32 {t2}, {a}, {a}, 22",
             f"v_bitop3_b32 {t0}, {t0}, {t1}, {t2} bitop3:0x96",
             f"v_bitop3_b32 {t1}, {a}, {b}, {c} bitop3:0xe8",
-            f"v_add3_u32 {h}, {h}, {t0}, {t1}",
         ]
+        if add_mode == "add3":
+            lines.append(f"v_add3_u32 {h}, {h}, {t0}, {t1}")
+        else:
+            lines += [f"v_add_u32_e32 {h}, {h}, {t0}", f"v_add_u32_e32 {h}, {h}, {t1}"]
     return lines
+
+
+def block_ilp(j0):
+    """Latency-oriented order for waves that run alone on a SIMD (few long
+    chains, e.g. batch digests): h+K+W first, the e- and a-side rotations
+    interleaved, and the schedule word W[j+2] woven into round j, so no
+    instruction waits on the one right before it."""
+    R = [op(24 + i) for i in range(8)]
+    Q = [op(32 + i) for i in range(4)]
+    kop = lambda r: op(36 + r)
+    lines = []
+    for r in range(8):
+        j = j0 + r
+        a, b, c, d, e, f, g, h = [op(STATE[(k - r) % 8]) for k in range(8)]
+        wj = op(W[j & 15])
+        t = j + 2
+        sched = 16 <= t <= 63
+        if sched:
+            wt, wt2, wt7, wt15 = op(W[t & 15]), op(W[(t - 2) & 15]), op(W[(t - 7) & 15]), op(W[(t - 15) & 15])
+        S = lambda ins: lines.append(ins) if sched else None
+        lines.append(f"v_add3_u32 {h}, {h}, {kop(r)}, {wj}")
+        lines.append(f"v_alignbit_b32 {R[0]}, {e}, {e}, 6")
+        if sched: S(f"v_alignbit_b32 {Q[0]}, {wt15}, {wt15}, 7")
+        lines.append(f"v_alignbit_b32 {R[1]}, {e}, {e}, 11")
+        if sched: S(f"v_alignbit_b32 {Q[1]}, {wt15}, {wt15}, 18")
+        lines.append(f"v_alignbit_b32 {R[2]}, {e}, {e}, 25")
+        if sched: S(f"v_lshrrev_b32_e32 {Q[2]}, 3, {wt15}")
+        lines.append(f"v_bitop3_b32 {R[3]}, {e}, {f}, {g} bitop3:0xca")
+        lines.append(f"v_alignbit_b32 {R[4]}, {a}, {a}, 2")
+        if sched: S(f"v_bitop3_b32 {Q[0]}, {Q[0]}, {Q[1]}, {Q[2]} bitop3:0x96")
+        lines.append(f"v_bitop3_b32 {R[0]}, {R[0]}, {R[1]}, {R[2]} bitop3:0x96")
+        lines.append(f"v_alignbit_b32 {R[5]}, {a}, {a}, 13")
+        if sched: S(f"v_alignbit_b32 {Q[1]}, {wt2}, {wt2}, 17")
+        lines.append(f"v_add3_u32 {h}, {h}, {R[0]}, {R[3]}")
+        lines.append(f"v_alignbit_b32 {R[6]}, {a}, {a}, 22")
+        if sched: S(f"v_alignbit_b32 {Q[2]}, {wt2}, {wt2}, 19")
+        lines.append(f"v_add_u32_e32 {d}, {d}, {h}")
+        lines.append(f"v_bitop3_b32 {R[7]}, {a}, {b}, {c} bitop3:0xe8")
+        if sched: S(f"v_lshrrev_b32_e32 {Q[3]}, 10, {wt2}")
+        lines.append(f"v_bitop3_b32 {R[4]}, {R[4]}, {R[5]}, {R[6]} bitop3:0x96")
+        if sched: S(f"v_bitop3_b32 {Q[1]}, {Q[1]}, {Q[2]}, {Q[3]} bitop3:0x96")
+        lines.append(f"v_add3_u32 {h}, {h}, {R[4]}, {R[7]}")
+        if sched:
+            S(f"v_add3_u32 {wt}, {wt}, {Q[0]}, {Q[1]}")
+            S(f"v_add_u32_e32 {wt}, {wt}, {wt7}")
+    return lines
+
+
+def emit_fn_ilp(name):
+    out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16]) {{",
+           "    uint32_t r0, r1, r2, r3, r4, r5, r6, r7, q0, q1, q2, q3;"]
+    for j0 in range(0, 64, 8):
+        body = block_ilp(j0)
+        out.append(f"    // rounds {j0}..{j0 + 7} (W[{j0 + 2}..{j0 + 9}] scheduled inside)")
+        out.append("    asm volatile(")
+        for ln in body:
+            out.append(f'        "{ln}\\n\\t"')
+        outs = ", ".join([f'"+v"(s[{i}])' for i in range(8)] + [f'"+v"(w[{i}])' for i in range(16)]
+                         + [f'"=&v"(r{i})' for i in range(8)] + [f'"=&v"(q{i})' for i in range(4)])
+        ins = ", ".join(f'"s"(0x{K[j0 + r]:08X}u)' for r in range(8))
+        out.append(f"        : {outs}")
+        out.append(f"        : {ins});")
+    out.append("}")
+    out.append("")
+    return out
+
+
+VARIANTS = {
+    # name: (ch_mode, add_mode, k_mode)
+    "rounds_asm": ("bitop3", "add3", "sgpr"),
+    "rounds_asm_bfi": ("bfi", "add3", "sgpr"),
+    "rounds_asm_add2": ("bitop3", "add", "sgpr"),
+    "rounds_asm_lit": ("bitop3", "add3", "lit"),
+    "rounds_asm_add2lit": ("bitop3", "add", "lit"),
+}
+
+
+def emit_fn(name, ch_mode, add_mode, k_mode):
+    out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16]) {{",
+           "    uint32_t t0, t1, t2, t3;"]
+    for j0 in range(0, 64, 8):
+        body = block(j0, ch_mode, add_mode, k_mode)
+        out.append(f"    // rounds {j0}..{j0 + 7}")
+        out.append("    asm volatile(")
+        for ln in body:
+            out.append(f'        "{ln}\\n\\t"')
+        outs = ", ".join([f'"+v"(s[{i}])' for i in range(8)] + [f'"+v"(w[{i}])' for i in range(16)]
+                         + ['"=&v"(t0)', '"=&v"(t1)', '"=&v"(t2)', '"=&v"(t3)'])
+        if k_mode == "sgpr":
+            ins = ", ".join(f'"s"(0x{K[j0 + r]:08X}u)' for r in range(8))
+        else:
+            ins = ""
+        out.append(f"        : {outs}")
+        out.append(f"        : {ins});")
+    out.append("}")
+    out.append("")
+    return out
 
 
 def emit():
     out = []
     out.append("// GENERATED by gen_rounds_asm.py — do not edit by hand.")
     out.append("// 64 SHA-256 rounds (FIPS 180-4 §6.2.2) for gfx950, 8 per asm statement.")
+    out.append("// rounds_asm is the production form; the others exist for A/B timing")
+    out.append("// (tools/valu_microbench.hip) and are bit-identical in result.")
     out.append("#pragma once")
     out.append("#include <stdint.h>")
     out.append("")
@@ -96,21 +212,10 @@ def emit():
     out.append("")
     out.append("// s[0..7] = working variables a..h (updated in place: after 8 rounds the")
     out.append("// names have rotated back), w[0..15] = schedule window (consumed).")
-    out.append("__device__ __forceinline__ void rounds_asm(uint32_t s[8], uint32_t w[16]) {")
-    out.append("    uint32_t t0, t1, t2, t3;")
-    for j0 in range(0, 64, 8):
-        body = block(j0)
-        out.append(f"    // rounds {j0}..{j0 + 7}")
-        out.append("    asm volatile(")
-        for ln in body:
-            out.append(f'        "{ln}\\n\\t"')
-        outs = ", ".join([f'"+v"(s[{i}])' for i in range(8)] + [f'"+v"(w[{i}])' for i in range(16)]
-                         + ['"=&v"(t0)', '"=&v"(t1)', '"=&v"(t2)', '"=&v"(t3)'])
-        ins = ", ".join(f'"s"(0x{K[j0 + r]:08X}u)' for r in range(8))
-        out.append(f"        : {outs}")
-        out.append(f"        : {ins});")
-    out.append("}")
-    out.append("")
+    for name, (ch, ad, km) in VARIANTS.items():
+        out += emit_fn(name, ch, ad, km)
+    out.append("// Latency-oriented order (lone waves): same instructions, 12 temporaries.")
+    out += emit_fn_ilp("rounds_asm_ilp")
     out.append("}  // namespace mirsha")
     return "\n".join(out) + "\n"
 

@@ -80,7 +80,7 @@ struct mirsha_ctx {
     int variant = mirsha::kVariantLds;
     bool timing = false;
     std::string err;
-    DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2;
+    DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
     PinnedBuf h_stage;
     KernelTimer timers[3];
 };
@@ -253,11 +253,13 @@ int hash_host_messages(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
 int check_lists(mirsha_ctx* c, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
                 uint32_t n_digests) {
     if (!first) return fail(c, MIRSHA_EINVAL, "list_first is NULL");
+    if (n_digests > mirsha::kMaxListDigests) return fail(c, MIRSHA_ERANGE, "%u digests > %u", n_digests, mirsha::kMaxListDigests);
     if (first[0] != 0) return fail(c, MIRSHA_EINVAL, "list_first[0] must be 0");
     for (uint32_t b = 0; b < n_lists; b++)
         if (first[b + 1] < first[b]) return fail(c, MIRSHA_EINVAL, "list_first not monotone at %u", b);
     const uint32_t entries = first[n_lists];
     if (entries && !idx) return fail(c, MIRSHA_EINVAL, "idx is NULL");
+    if (entries > mirsha::kMaxListEntries) return fail(c, MIRSHA_ERANGE, "%u list entries > %u", entries, mirsha::kMaxListEntries);
     for (uint32_t e = 0; e < entries; e++)
         if (idx[e] != MIRSHA_NULL_INDEX && idx[e] >= n_digests)
             return fail(c, MIRSHA_EINVAL, "idx[%u]=%u out of range (%u digests)", e, idx[e], n_digests);
@@ -269,7 +271,7 @@ int check_lists(mirsha_ctx* c, const uint32_t* idx, const uint32_t* first, uint3
 }
 
 // Digest lists over device-resident digests d_digests; writes d_out (device).
-int lists_resident(mirsha_ctx* c, const uint8_t* d_digests, const uint32_t* idx,
+int lists_resident(mirsha_ctx* c, const uint8_t* d_digests, uint32_t n_digests, const uint32_t* idx,
                    const uint32_t* first, uint32_t n_lists, uint8_t* d_out) {
     const uint32_t entries = first[n_lists];
     HIP_TRY(c, c->d_first.ensure(sizeof(uint32_t) * (n_lists + 1)));
@@ -277,9 +279,10 @@ int lists_resident(mirsha_ctx* c, const uint8_t* d_digests, const uint32_t* idx,
     HIP_TRY(c, hipMemcpyAsync(c->d_first.p, first, sizeof(uint32_t) * (n_lists + 1), hipMemcpyHostToDevice, c->stream));
     if (entries)
         HIP_TRY(c, hipMemcpyAsync(c->d_idx.p, idx, sizeof(uint32_t) * entries, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, c->d_scratch.ensure(sizeof(uint32_t) * std::max<uint32_t>(entries, 1)));
     return timed_launch(c, 1, [&] {
-        return mirsha::launch_lists(d_digests, c->d_idx.as<uint32_t>(), c->d_first.as<uint32_t>(),
-                                    n_lists, d_out, c->stream);
+        return mirsha::launch_lists(d_digests, n_digests, c->d_idx.as<uint32_t>(), entries, c->d_first.as<uint32_t>(),
+                                    n_lists, c->d_scratch.as<uint32_t>(), d_out, c->stream);
     });
 }
 
@@ -332,7 +335,7 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
         for (auto e : t.pool) (void)hipEventDestroy(e);
     }
     c->d_arena.release(); c->d_off.release(); c->d_len.release(); c->d_order.release();
-    c->d_out.release(); c->d_idx.release(); c->d_first.release(); c->d_out2.release();
+    c->d_out.release(); c->d_idx.release(); c->d_first.release(); c->d_out2.release(); c->d_scratch.release();
     c->h_stage.release();
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -480,7 +483,7 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
     if (int rc = hash_host_messages(c, arena, arena_len, off, len, n_req, c->d_out.as<uint8_t>())) return rc;
     if (n_batches) {
         HIP_TRY(c, c->d_out2.ensure(32ull * n_batches));
-        if (int rc = lists_resident(c, c->d_out.as<uint8_t>(), idx, first, n_batches, c->d_out2.as<uint8_t>()))
+        if (int rc = lists_resident(c, c->d_out.as<uint8_t>(), n_req, idx, first, n_batches, c->d_out2.as<uint8_t>()))
             return rc;
         HIP_TRY(c, hipMemcpyAsync(batch_out, c->d_out2.p, 32ull * n_batches, hipMemcpyDeviceToHost, c->stream));
     }
@@ -500,7 +503,8 @@ int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digest
     if (n_digests)
         HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, digests, 32ull * n_digests, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, c->d_out2.ensure(32ull * n_lists));
-    if (int rc = lists_resident(c, c->d_arena.as<uint8_t>(), idx, first, n_lists, c->d_out2.as<uint8_t>())) return rc;
+    if (int rc = lists_resident(c, c->d_arena.as<uint8_t>(), n_digests, idx, first, n_lists, c->d_out2.as<uint8_t>()))
+        return rc;
     HIP_TRY(c, hipMemcpyAsync(out, c->d_out2.p, 32ull * n_lists, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return MIRSHA_OK;
@@ -522,13 +526,19 @@ int mirsha_hash_batch_device(mirsha_ctx* c, const uint8_t* d_arena, uint64_t are
     });
 }
 
-int mirsha_digest_lists_device(mirsha_ctx* c, const uint8_t* d_digests, const uint32_t* d_idx,
-                               const uint32_t* d_first, uint32_t n_lists, uint8_t* d_out) {
+int mirsha_digest_lists_device(mirsha_ctx* c, const uint8_t* d_digests, uint32_t n_digests, const uint32_t* d_idx,
+                               const uint32_t* d_first, uint32_t n_lists, uint32_t n_entries, uint8_t* d_out) {
     if (!c) return MIRSHA_EINVAL;
     if (n_lists == 0) return MIRSHA_OK;
-    if (!d_digests || !d_idx || !d_first || !d_out) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (!d_idx || !d_first || !d_out) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (n_digests > mirsha::kMaxListDigests) return fail(c, MIRSHA_ERANGE, "n_digests %u too large", n_digests);
+    if (n_entries > mirsha::kMaxListEntries) return fail(c, MIRSHA_ERANGE, "n_entries %u too large", n_entries);
     if (int rc = use_device(c)) return rc;
-    return timed_launch(c, 1, [&] { return mirsha::launch_lists(d_digests, d_idx, d_first, n_lists, d_out, c->stream); });
+    HIP_TRY(c, c->d_scratch.ensure(sizeof(uint32_t) * std::max<uint32_t>(n_entries, 1)));
+    return timed_launch(c, 1, [&] {
+        return mirsha::launch_lists(d_digests, n_digests, d_idx, n_entries, d_first, n_lists,
+                                    c->d_scratch.as<uint32_t>(), d_out, c->stream);
+    });
 }
 
 int mirsha_bucket_order(const uint32_t* len, uint32_t n, uint32_t* order_out) {

@@ -16,8 +16,13 @@ enum : int { kVariantLds = 0, kVariantDirect = 1, kVariantLdsCxx = 2, kVariantDi
 hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t* off,
                        const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
                        int variant, hipStream_t s);
-hipError_t launch_lists(const uint8_t* digests, const uint32_t* idx, const uint32_t* first,
-                        uint32_t n_lists, uint8_t* out, hipStream_t s);
+// scratch: device buffer with at least first[n_lists] entries (null compaction).
+// Digest reads are range-checked against n_digests (out-of-range reads zeros).
+constexpr uint32_t kMaxListDigests = (1u << 27) - 1u;
+// Index reads are range-checked against n_entries (= first[n_lists]).
+constexpr uint32_t kMaxListEntries = (1u << 30) - 1u;
+hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32_t* idx, uint32_t n_entries,
+                        const uint32_t* first, uint32_t n_lists, uint32_t* scratch, uint8_t* out, hipStream_t s);
 hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
                                uint8_t* arena, hipStream_t s);
 

@@ -199,15 +199,67 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
 
 // Dependent pass: message k = concat(digests[idx[e]] for e in [first[k], first[k+1]))
 // skipping idx == kNullIndex (a null request's empty digest, client_tracker.go:840-847).
+// One lane per list.  These waves run few per SIMD, so every global read on
+// the chain is an unconditional, range-checked buffer load (no branch + wait
+// per element): indices are prefetched two blocks ahead, digests one block
+// ahead.  If any list of the wave holds null entries, the whole wave first
+// compacts its lists into `scratch` (same positions as idx) and reads there.
+// aux bit 31 (volatile) keeps hipcc from merging adjacent dword loads into a
+// dwordx2/x4, whose range check would zero in-range entries that share an
+// access with out-of-range ones at the end of the array (lowers to sc0 sc1:
+// L1 bypass, L2-served).
+constexpr int kNoMerge = (int)(1u << 31);
+__device__ __forceinline__ uint32_t ld_u32(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool live) {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, live ? off : 0xFFFFFFF0u, 0, kNoMerge);
+}
+
+// Digest `id` through a range-checked descriptor: a dead slot (or an index
+// past n_digests) reads zeros instead of faulting, without a branch.
+__device__ __forceinline__ void load_digest(__amdgpu_buffer_rsrc_t rsrc, uint32_t id, bool live, uint4& x0,
+                                            uint4& x1) {
+    const uint32_t o = live ? 32u * id : 0xFFFFFFE0u;
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, 0);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16u, 0, 0);
+    x0 = make_uint4(a[0], a[1], a[2], a[3]);
+    x1 = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
 __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
-    const uint8_t* __restrict__ digests, const uint32_t* __restrict__ idx,
-    const uint32_t* __restrict__ first, uint32_t n_lists, uint8_t* __restrict__ out) {
+    const uint8_t* __restrict__ digests, uint32_t n_digests, const uint32_t* __restrict__ idx,
+    uint32_t n_entries, const uint32_t* __restrict__ first, uint32_t n_lists, uint32_t* __restrict__ scratch,
+    uint8_t* __restrict__ out) {
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)idx, (short)0, (int)(4u * n_entries), 0x00020000);
     const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
     const bool valid = k < n_lists;
     const uint32_t e0 = valid ? first[k] : 0u;
     const uint32_t e1 = valid ? first[k + 1] : 0u;
-    uint32_t c = 0;  // non-null entries
-    for (uint32_t e = e0; e < e1; e++) c += idx[e] != kNullIndex;
+
+    // Prologue: count non-null entries, 8 unconditional loads per round.
+    uint32_t c = 0;
+    for (uint32_t e = e0; e < e1; e += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b32(irs, 4u * (e + i), 0, kNoMerge);
+#pragma unroll
+        for (int i = 0; i < 8; i++) c += (e + i < e1) && v[i] != kNullIndex;
+    }
+    const bool any_null = __any(c != e1 - e0);  // wave-uniform
+    __amdgpu_buffer_rsrc_t brs = irs;
+    if (any_null) {
+        // Whole wave: this lane's non-null entries to scratch[e0 .. e0+c).
+        uint32_t m = 0;
+        for (uint32_t e = e0; e < e1; e++) {
+            const uint32_t v = idx[e];
+            if (v != kNullIndex) scratch[e0 + m++] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        brs = __builtin_amdgcn_make_buffer_rsrc((void*)scratch, (short)0, (int)(4u * n_entries), 0x00020000);
+    }
+
     const uint32_t L = 32u * c;
     const uint32_t nb = valid ? blocks_for_len(L) : 0u;
     const uint32_t wave_nb = wave_max(nb);
@@ -215,27 +267,34 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
     uint32_t st[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] = kH0[i];
-    uint32_t cur = e0;  // cursor over the index list
+
+    // Pipeline registers: digests of block b (cur), indices of block b+1 (nx).
+    uint4 cur[4];
+    uint32_t nx0 = ld_u32(brs, 4u * (e0 + 2u), 2u < c), nx1 = ld_u32(brs, 4u * (e0 + 3u), 3u < c);
+    {
+        const uint32_t i0 = ld_u32(brs, 4u * e0, 0u < c), i1 = ld_u32(brs, 4u * (e0 + 1u), 1u < c);
+        load_digest(drs, i0, 0u < c, cur[0], cur[1]);
+        load_digest(drs, i1, 1u < c, cur[2], cur[3]);
+    }
     for (uint32_t blk = 0; blk < wave_nb; blk++) {
+        // Issue block b+1's digests and block b+2's indices before compressing b.
+        uint4 nxt[4];
+        load_digest(drs, nx0, 2u * blk + 2u < c, nxt[0], nxt[1]);
+        load_digest(drs, nx1, 2u * blk + 3u < c, nxt[2], nxt[3]);
+        const uint32_t nn0 = ld_u32(brs, 4u * (e0 + 2u * blk + 4u), 2u * blk + 4u < c);
+        const uint32_t nn1 = ld_u32(brs, 4u * (e0 + 2u * blk + 5u), 2u * blk + 5u < c);
         if (blk < nb) {
             uint32_t w[16];
 #pragma unroll
             for (int half = 0; half < 2; half++) {
                 const uint32_t di = 2u * blk + (uint32_t)half;  // digest ordinal in the message
-                if (di < c) {
-                    while (idx[cur] == kNullIndex) cur++;
-                    const uint4* src = reinterpret_cast<const uint4*>(digests + 32ull * idx[cur]);
-                    cur++;
-                    const uint4 x0 = src[0], x1 = src[1];
-                    w[8 * half + 0] = __builtin_bswap32(x0.x); w[8 * half + 1] = __builtin_bswap32(x0.y);
-                    w[8 * half + 2] = __builtin_bswap32(x0.z); w[8 * half + 3] = __builtin_bswap32(x0.w);
-                    w[8 * half + 4] = __builtin_bswap32(x1.x); w[8 * half + 5] = __builtin_bswap32(x1.y);
-                    w[8 * half + 6] = __builtin_bswap32(x1.z); w[8 * half + 7] = __builtin_bswap32(x1.w);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) w[8 * half + i] = 0u;
-                    if (di == c) w[8 * half] = 0x80000000u;
-                }
+                const uint4 x0 = cur[2 * half], x1 = cur[2 * half + 1];
+                // Past the end the loads returned zeros; only the 0x80 marker is added.
+                w[8 * half + 0] = __builtin_bswap32(x0.x) | (di == c ? 0x80000000u : 0u);
+                w[8 * half + 1] = __builtin_bswap32(x0.y); w[8 * half + 2] = __builtin_bswap32(x0.z);
+                w[8 * half + 3] = __builtin_bswap32(x0.w); w[8 * half + 4] = __builtin_bswap32(x1.x);
+                w[8 * half + 5] = __builtin_bswap32(x1.y); w[8 * half + 6] = __builtin_bswap32(x1.z);
+                w[8 * half + 7] = __builtin_bswap32(x1.w);
             }
             if (blk + 1u == nb) {
                 w[14] = L >> 29;
@@ -243,6 +302,10 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
             }
             compress_asm(st, w);
         }
+#pragma unroll
+        for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+        nx0 = nn0;
+        nx1 = nn1;
     }
     if (valid) store_digest(out, k, st);
 }
@@ -302,11 +365,12 @@ hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t*
     return hipGetLastError();
 }
 
-hipError_t launch_lists(const uint8_t* digests, const uint32_t* idx, const uint32_t* first,
-                        uint32_t n_lists, uint8_t* out, hipStream_t s) {
+hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32_t* idx, uint32_t n_entries,
+                        const uint32_t* first, uint32_t n_lists, uint32_t* scratch, uint8_t* out, hipStream_t s) {
     if (n_lists == 0) return hipSuccess;
     const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
-    sha256_lists_kernel<<<grid, kBlockThreads, 0, s>>>(digests, idx, first, n_lists, out);
+    sha256_lists_kernel<<<grid, kBlockThreads, 0, s>>>(digests, n_digests, idx, n_entries, first, n_lists, scratch,
+                                                      out);
     return hipGetLastError();
 }
 

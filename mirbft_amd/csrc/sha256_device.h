@@ -83,6 +83,16 @@ __device__ __forceinline__ void compress_asm(uint32_t st[8], uint32_t w[16]) {
     for (int i = 0; i < 8; i++) st[i] += s[i];
 }
 
+// Same, latency-oriented round order (for waves alone on their SIMD).
+__device__ __forceinline__ void compress_asm_ilp(uint32_t st[8], uint32_t w[16]) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = st[i];
+    rounds_asm_ilp(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] += s[i];
+}
+
 // Number of 64-byte compressions for an L-byte message: ceil((L + 9) / 64).
 __device__ __host__ __forceinline__ uint32_t blocks_for_len(uint32_t L) { return (L + 72u) >> 6; }
 

@@ -186,8 +186,10 @@ class Engine:
                           n: int, d_out: int) -> None:
         self._check(self._lib.mirsha_hash_batch_device(self.ctx, d_arena, arena_len, d_off, d_len, d_order, n, d_out))
 
-    def digest_lists_device(self, d_digests: int, d_idx: int, d_first: int, n_lists: int, d_out: int) -> None:
-        self._check(self._lib.mirsha_digest_lists_device(self.ctx, d_digests, d_idx, d_first, n_lists, d_out))
+    def digest_lists_device(self, d_digests: int, n_digests: int, d_idx: int, d_first: int, n_lists: int,
+                            n_entries: int, d_out: int) -> None:
+        self._check(self._lib.mirsha_digest_lists_device(self.ctx, d_digests, n_digests, d_idx, d_first, n_lists,
+                                                         n_entries, d_out))
 
     def synth_requests_device(self, seed: int, first: int, count: int, data_len: int, d_arena: int) -> None:
         self._check(self._lib.mirsha_synth_requests_device(self.ctx, seed, first, count, data_len, d_arena))

@@ -295,7 +295,8 @@ def test_full_size_configs_device_resident(engine, cfg, data_len, n, bs):
     engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
     engine.hash_batch_device(d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr(), None, n,
                              d_req.data_ptr())
-    engine.digest_lists_device(d_req.data_ptr(), d_idx.data_ptr(), d_first.data_ptr(), nb, d_bat.data_ptr())
+    engine.digest_lists_device(d_req.data_ptr(), n, d_idx.data_ptr(), d_first.data_ptr(), nb, int(first[-1]),
+                               d_bat.data_ptr())
     engine.sync()
     arena = oracle_py.gen_requests(seed, 0, n, data_len)
     want_req = oracle_py.hash_requests(arena, np.arange(n, dtype=np.uint64) * stride, np.full(n, stride), threads=8)
@@ -351,3 +352,24 @@ def test_device_order_permutation(engine):
                              d_out.data_ptr())
     engine.sync()
     assert np.array_equal(d_out.cpu().numpy(), oracle_py.hash_requests(arena, off, lens))
+
+
+def test_device_lists_with_nulls_and_empty(engine):
+    """Device digest-list API: null entries (compaction path), empty lists, odd/even counts."""
+    torch = _torch()
+    rng = np.random.default_rng(12)
+    nd = 777
+    dig = rng.integers(0, 256, (nd, 32), dtype=np.uint8)
+    sizes = rng.integers(0, 45, 1500)
+    sizes[::7] = 0
+    idx = rng.integers(0, nd, int(sizes.sum())).astype(np.uint32)
+    idx[rng.random(idx.size) < 0.15] = _lib.MIRSHA_NULL_INDEX
+    first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    d_dig = torch.from_numpy(dig).cuda()
+    d_idx = torch.from_numpy(idx.view(np.int32)).cuda()
+    d_first = torch.from_numpy(first.view(np.int32)).cuda()
+    d_out = torch.empty((sizes.size, 32), dtype=torch.uint8, device="cuda")
+    engine.digest_lists_device(d_dig.data_ptr(), nd, d_idx.data_ptr(), d_first.data_ptr(), sizes.size,
+                               int(first[-1]), d_out.data_ptr())
+    engine.sync()
+    assert np.array_equal(d_out.cpu().numpy(), oracle_py.batch_digests(dig, idx, first))

@@ -53,6 +53,22 @@ constexpr int ITERS = 2048;
 #define OP_ADDLSHL(i) "v_add_lshl_u32 %" #i ", %" #i ", %8, 3\n\t"
 #define OP_LSHLREV(i) "v_lshlrev_b32_e32 %" #i ", 7, %" #i "\n\t"
 #define OP_ADD3SV(i) "v_add3_u32 %" #i ", %" #i ", %9, %8\n\t" "v_add_u32_e32 %" #i ", %" #i ", %8\n\t"
+// T2: independent simple/complex alternation (chains 0..7 all different)
+#define T2BODY "v_add_u32_e32 %0, %0, %8\n\tv_alignbit_b32 %1, %1, %1, 7\n\tv_add_u32_e32 %2, %2, %8\n\tv_alignbit_b32 %3, %3, %3, 7\n\tv_add_u32_e32 %4, %4, %8\n\tv_alignbit_b32 %5, %5, %5, 7\n\tv_add_u32_e32 %6, %6, %8\n\tv_alignbit_b32 %7, %7, %7, 7\n\t"
+// T3: dependent adds (one chain per statement position, consecutive instructions dependent)
+#define T3BODY "v_add_u32_e32 %0, %0, %8\n\tv_add_u32_e32 %0, %0, %8\n\tv_add_u32_e32 %0, %0, %8\n\tv_add_u32_e32 %0, %0, %8\n\tv_add_u32_e32 %1, %1, %8\n\tv_add_u32_e32 %1, %1, %8\n\tv_add_u32_e32 %1, %1, %8\n\tv_add_u32_e32 %1, %1, %8\n\t"
+// T4: simple pairs then complex pairs: add a, add b, align c, align d
+#define T4BODY "v_add_u32_e32 %0, %0, %8\n\tv_add_u32_e32 %1, %1, %8\n\tv_alignbit_b32 %2, %2, %2, 7\n\tv_alignbit_b32 %3, %3, %3, 7\n\tv_add_u32_e32 %4, %4, %8\n\tv_add_u32_e32 %5, %5, %8\n\tv_alignbit_b32 %6, %6, %6, 7\n\tv_alignbit_b32 %7, %7, %7, 7\n\t"
+// T5: dependent bitop3 chain
+#define T5BODY "v_bitop3_b32 %0, %0, %8, %10 bitop3:0x96\n\tv_bitop3_b32 %0, %0, %8, %10 bitop3:0x96\n\tv_bitop3_b32 %0, %0, %8, %10 bitop3:0x96\n\tv_bitop3_b32 %0, %0, %8, %10 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %10 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %10 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %10 bitop3:0x96\n\tv_bitop3_b32 %1, %1, %8, %10 bitop3:0x96\n\t"
+// T6: 3 simple (add, bitop3, xor) independent, then 1 complex
+#define T6BODY "v_add_u32_e32 %0, %0, %8\n\tv_bitop3_b32 %1, %1, %8, %10 bitop3:0x96\n\tv_xor_b32_e32 %2, %2, %8\n\tv_alignbit_b32 %3, %3, %3, 7\n\tv_add_u32_e32 %4, %4, %8\n\tv_bitop3_b32 %5, %5, %8, %10 bitop3:0x96\n\tv_xor_b32_e32 %6, %6, %8\n\tv_alignbit_b32 %7, %7, %7, 7\n\t"
+#define RAWBODY(STR) asm volatile(STR : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]) : "v"(y), "s"(k), "v"(z));
+#define OP_LSHR7(i) "v_lshrrev_b32_e32 %" #i ", 7, %" #i "\n\t"
+#define OP_LSHL3(i) "v_lshlrev_b32_e32 %" #i ", 3, %" #i "\n\t"
+#define OP_LSHLV(i) "v_lshlrev_b32_e32 %" #i ", %8, %" #i "\n\t"
+#define OP_OR(i) "v_or_b32_e32 %" #i ", %" #i ", %8\n\t"
+#define OP_SUB(i) "v_sub_u32_e32 %" #i ", %" #i ", %8\n\t"
 #define OP_MIXAA(i) "v_alignbit_b32 %" #i ", %" #i ", %" #i ", 7\n\t" "v_add_u32_e32 %" #i ", %" #i ", %8\n\t"
 
 template <int KIND>
@@ -90,6 +106,16 @@ __global__ __launch_bounds__(256) void mb(unsigned* out, unsigned long long* clk
             if constexpr (KIND == 19) BODY(OP_LSHLREV)
             if constexpr (KIND == 20) BODY(OP_ADD3SV)
             if constexpr (KIND == 21) BODY(OP_MIXAA)
+            if constexpr (KIND == 22) RAWBODY(T2BODY)
+            if constexpr (KIND == 23) RAWBODY(T3BODY)
+            if constexpr (KIND == 24) RAWBODY(T4BODY)
+            if constexpr (KIND == 25) RAWBODY(T5BODY)
+            if constexpr (KIND == 26) RAWBODY(T6BODY)
+            if constexpr (KIND == 27) BODY(OP_LSHR7)
+            if constexpr (KIND == 28) BODY(OP_LSHL3)
+            if constexpr (KIND == 29) BODY(OP_LSHLV)
+            if constexpr (KIND == 30) BODY(OP_OR)
+            if constexpr (KIND == 31) BODY(OP_SUB)
         }
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
@@ -139,7 +165,22 @@ void run(const char* name, int blocks, unsigned* d_out, unsigned long long* d_cl
 
 // Pure-register SHA-256 compression loop (generated-asm rounds): the
 // achievable per-compression cost with no memory traffic at all.
-template <bool kAsm>
+template <int V>
+__device__ __forceinline__ void compress_variant(uint32_t st[8], uint32_t w[16]) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = st[i];
+    if constexpr (V == 0) mirsha::rounds_asm(s, w);
+    if constexpr (V == 1) mirsha::rounds_asm_bfi(s, w);
+    if constexpr (V == 2) mirsha::rounds_asm_add2(s, w);
+    if constexpr (V == 3) mirsha::rounds_asm_lit(s, w);
+    if constexpr (V == 4) mirsha::rounds_asm_add2lit(s, w);
+    if constexpr (V == 5) mirsha::rounds_asm_ilp(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] += s[i];
+}
+
+template <int kAsm>
 __global__ __launch_bounds__(256) void sha_loop(unsigned* out, unsigned long long* clk, int nblk) {
     uint32_t st[8], w[16];
 #pragma unroll
@@ -148,7 +189,7 @@ __global__ __launch_bounds__(256) void sha_loop(unsigned* out, unsigned long lon
     for (int b = 0; b < nblk; b++) {
 #pragma unroll
         for (int i = 0; i < 16; i++) w[i] = st[i & 7] + i;
-        if constexpr (kAsm) mirsha::compress_asm(st, w); else mirsha::compress(st, w);
+        if constexpr (kAsm >= 0) compress_variant<kAsm>(st, w); else mirsha::compress(st, w);
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     out[blockIdx.x * blockDim.x + threadIdx.x] = st[0] ^ st[7];
@@ -158,7 +199,7 @@ __global__ __launch_bounds__(256) void sha_loop(unsigned* out, unsigned long lon
     }
 }
 
-template <bool kAsm>
+template <int kAsm>
 void run_sha1(int blocks, unsigned* d_out, unsigned long long* d_clk, int wpb) {
     const int nblk = 256;
     hipEvent_t e0, e1;
@@ -187,13 +228,16 @@ void run_sha1(int blocks, unsigned* d_out, unsigned long long* d_clk, int wpb) {
     const double per_simd_wave_blocks = comps / 64.0 / 1024.0;
     printf("{\"op\": \"sha256_compress_%s\", \"waves_per_simd\": %d, \"ms\": %.4f, \"clock_ghz\": %.3f, "
            "\"gcompress_per_s\": %.2f, \"cycles_per_wave_compress\": %.1f}\n",
-           kAsm ? "asm" : "cxx", wpb, best, ghz, comps / (best * 1e-3) / 1e9,
+           kAsm == 0 ? "asm" : kAsm == 1 ? "asm_bfi" : kAsm == 2 ? "asm_add2" : kAsm == 3 ? "asm_lit" : kAsm == 4 ? "asm_add2lit" : kAsm == 5 ? "asm_ilp" : "cxx", wpb, best, ghz, comps / (best * 1e-3) / 1e9,
            best * 1e-3 * ghz * 1e9 / per_simd_wave_blocks);
 }
 
 void run_sha(int blocks, unsigned* d_out, unsigned long long* d_clk) {
-    for (int wpb : {2, 4, 8}) run_sha1<true>(blocks, d_out, d_clk, wpb);
-    run_sha1<false>(blocks, d_out, d_clk, 8);
+    for (int wps : {8, 2, 1}) {
+        run_sha1<0>(blocks, d_out, d_clk, wps);
+        run_sha1<5>(blocks, d_out, d_clk, wps);
+        run_sha1<-1>(blocks, d_out, d_clk, wps);
+    }
 }
 
 int main() {
@@ -224,6 +268,16 @@ int main() {
     run<19>("v_lshlrev_b32", blocks, d_out, d_clk);
     run<20>("mix add3(sgpr)+add", blocks, d_out, d_clk);
     run<21>("mix alignbit+add", blocks, d_out, d_clk);
-    run_sha(blocks, d_out, d_clk);
+    run<22>("T2 add|align alternating, independent", blocks, d_out, d_clk);
+    run<23>("T3 dependent adds", blocks, d_out, d_clk);
+    run<24>("T4 add,add,align,align independent", blocks, d_out, d_clk);
+    run<25>("T5 dependent bitop3", blocks, d_out, d_clk);
+    run<26>("T6 add,bitop3,xor,align independent", blocks, d_out, d_clk);
+    run<27>("v_lshrrev_b32 7", blocks, d_out, d_clk);
+    run<28>("v_lshlrev_b32 3", blocks, d_out, d_clk);
+    run<29>("v_lshlrev_b32 vgpr", blocks, d_out, d_clk);
+    run<30>("v_or_b32", blocks, d_out, d_clk);
+    run<31>("v_sub_u32", blocks, d_out, d_clk);
+    if (getenv("MB_SHA")) run_sha(blocks, d_out, d_clk);
     return 0;
 }
