@@ -224,63 +224,34 @@ __device__ __forceinline__ void load_digest(__amdgpu_buffer_rsrc_t rsrc, uint32_
     x1 = make_uint4(b[0], b[1], b[2], b[3]);
 }
 
-__global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
-    const uint8_t* __restrict__ digests, uint32_t n_digests, const uint32_t* __restrict__ idx,
-    uint32_t n_entries, const uint32_t* __restrict__ first, uint32_t n_lists, uint32_t* __restrict__ scratch,
-    uint8_t* __restrict__ out) {
-    const __amdgpu_buffer_rsrc_t drs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
-    const __amdgpu_buffer_rsrc_t irs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)idx, (short)0, (int)(4u * n_entries), 0x00020000);
-    const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
-    const bool valid = k < n_lists;
-    const uint32_t e0 = valid ? first[k] : 0u;
-    const uint32_t e1 = valid ? first[k + 1] : 0u;
-
-    // Prologue: count non-null entries, 8 unconditional loads per round.
-    uint32_t c = 0;
-    for (uint32_t e = e0; e < e1; e += 8) {
-        uint32_t v[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) v[i] = __builtin_amdgcn_raw_buffer_load_b32(irs, 4u * (e + i), 0, kNoMerge);
-#pragma unroll
-        for (int i = 0; i < 8; i++) c += (e + i < e1) && v[i] != kNullIndex;
-    }
-    const bool any_null = __any(c != e1 - e0);  // wave-uniform
-    __amdgpu_buffer_rsrc_t brs = irs;
-    if (any_null) {
-        // Whole wave: this lane's non-null entries to scratch[e0 .. e0+c).
-        uint32_t m = 0;
-        for (uint32_t e = e0; e < e1; e++) {
-            const uint32_t v = idx[e];
-            if (v != kNullIndex) scratch[e0 + m++] = v;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        brs = __builtin_amdgcn_make_buffer_rsrc((void*)scratch, (short)0, (int)(4u * n_entries), 0x00020000);
-    }
-
+// Hash this lane's list whose non-null entries are read through `brs` at
+// [e0, e0 + c).  Returns true if a null marker was met (only possible on the
+// optimistic pass, where brs is the caller's idx and c = e1 - e0).
+__device__ __forceinline__ bool hash_list(__amdgpu_buffer_rsrc_t drs, __amdgpu_buffer_rsrc_t brs, uint32_t e0,
+                                          uint32_t c, bool valid, uint32_t st[8]) {
     const uint32_t L = 32u * c;
     const uint32_t nb = valid ? blocks_for_len(L) : 0u;
     const uint32_t wave_nb = wave_max(nb);
-
-    uint32_t st[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    bool saw_null = false;
 
     // Pipeline registers: digests of block b (cur), indices of block b+1 (nx).
     uint4 cur[4];
     uint32_t nx0 = ld_u32(brs, 4u * (e0 + 2u), 2u < c), nx1 = ld_u32(brs, 4u * (e0 + 3u), 3u < c);
     {
         const uint32_t i0 = ld_u32(brs, 4u * e0, 0u < c), i1 = ld_u32(brs, 4u * (e0 + 1u), 1u < c);
+        saw_null |= (0u < c && i0 == kNullIndex) || (1u < c && i1 == kNullIndex);
         load_digest(drs, i0, 0u < c, cur[0], cur[1]);
         load_digest(drs, i1, 1u < c, cur[2], cur[3]);
     }
     for (uint32_t blk = 0; blk < wave_nb; blk++) {
         // Issue block b+1's digests and block b+2's indices before compressing b.
+        const bool l0 = 2u * blk + 2u < c, l1 = 2u * blk + 3u < c;
+        saw_null |= (l0 && nx0 == kNullIndex) || (l1 && nx1 == kNullIndex);
         uint4 nxt[4];
-        load_digest(drs, nx0, 2u * blk + 2u < c, nxt[0], nxt[1]);
-        load_digest(drs, nx1, 2u * blk + 3u < c, nxt[2], nxt[3]);
+        load_digest(drs, nx0, l0, nxt[0], nxt[1]);
+        load_digest(drs, nx1, l1, nxt[2], nxt[3]);
         const uint32_t nn0 = ld_u32(brs, 4u * (e0 + 2u * blk + 4u), 2u * blk + 4u < c);
         const uint32_t nn1 = ld_u32(brs, 4u * (e0 + 2u * blk + 5u), 2u * blk + 5u < c);
         if (blk < nb) {
@@ -306,6 +277,40 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
         for (int i = 0; i < 4; i++) cur[i] = nxt[i];
         nx0 = nn0;
         nx1 = nn1;
+    }
+    return saw_null;
+}
+
+__global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
+    const uint8_t* __restrict__ digests, uint32_t n_digests, const uint32_t* __restrict__ idx,
+    uint32_t n_entries, const uint32_t* __restrict__ first, uint32_t n_lists, uint32_t* __restrict__ scratch,
+    uint8_t* __restrict__ out) {
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)idx, (short)0, (int)(4u * n_entries), 0x00020000);
+    const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
+    const bool valid = k < n_lists;
+    const uint32_t e0 = valid ? first[k] : 0u;
+    const uint32_t e1 = valid ? first[k + 1] : 0u;
+
+    // Optimistic pass: assume no null request in the list (the common case;
+    // no counting prologue on the latency chain).  Nulls are detected as the
+    // indices stream in; if any lane of the wave met one, the whole wave
+    // compacts its lists into scratch and hashes again (wave-uniform branch).
+    uint32_t st[8];
+    const bool saw_null = hash_list(drs, irs, e0, e1 - e0, valid, st);
+    if (__any(saw_null)) {
+        uint32_t m = 0;
+        for (uint32_t e = e0; e < e1; e++) {
+            const uint32_t v = idx[e];
+            if (v != kNullIndex) scratch[e0 + m++] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const __amdgpu_buffer_rsrc_t srs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)scratch, (short)0, (int)(4u * n_entries), 0x00020000);
+        (void)hash_list(drs, srs, e0, m, valid, st);
     }
     if (valid) store_digest(out, k, st);
 }

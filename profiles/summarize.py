@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Summarize a profiles/profile.sh output directory: per-kernel average
+duration (kernel trace) and per-launch PMC counter averages, with the gfx950
+corrections of MI355X_MICROARCH.md §HBM (FETCH_SIZE x2 for wide streaming
+reads; WRITE_SIZE as read) and the effective clock GRBM_GUI_ACTIVE / 8 / time."""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def short(name):
+    for k in ("sha256_msgs_kernel", "sha256_lists_kernel", "gen_requests_kernel"):
+        if k in name:
+            return k
+    return None
+
+
+def main(d):
+    out = {"kernels": {}}
+    stats = os.path.join(d, "trace", "run_kernel_stats.csv")
+    for r in csv.DictReader(open(stats)):
+        k = short(r["Name"])
+        if k:
+            out["kernels"].setdefault(k, {})["avg_ns"] = float(r["AverageNs"])
+            out["kernels"][k]["calls"] = int(r["Calls"])
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mem"):
+        f = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if k:
+                agg[(k, r["Counter_Name"])].append(float(r["Counter_Value"]))
+        for (k, c), v in agg.items():
+            out["kernels"].setdefault(k, {})[c] = sum(v) / len(v)
+    for k, v in out["kernels"].items():
+        t = v.get("avg_ns")
+        if "FETCH_SIZE" in v:
+            v["hbm_read_bytes_corrected"] = v["FETCH_SIZE"] * 1024 * 2  # KB units, x2 gfx950 correction
+        if "WRITE_SIZE" in v:
+            v["hbm_write_bytes"] = v["WRITE_SIZE"] * 1024
+        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
+            v["hbm_bytes_per_launch"] = v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
+        if t and "GRBM_GUI_ACTIVE" in v:
+            v["effective_clock_ghz"] = v["GRBM_GUI_ACTIVE"] / 8 / t
+        if "SQ_WAVE_CYCLES" in v:
+            wc = v["SQ_WAVE_CYCLES"]
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in v:
+                    v[c + "_frac"] = v[c] / wc
+        if "SQ_INSTS_VALU" in v and "SQ_WAVES" in v:
+            v["valu_insts_per_wave"] = v["SQ_INSTS_VALU"] / v["SQ_WAVES"]
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
