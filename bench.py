@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mirbft_amd import Engine, sharding  # noqa: E402
-from mirbft_amd.engine import KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
+from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
 
 SEED_BASE = 0x6D69726266740000
 # Algorithmic work unit: one 64-byte SHA-256 compression = 1384 int32 VALU ops
@@ -59,6 +59,12 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline sample (0 disables)")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-API measurement")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--pipeline", type=int, default=0,
+                   help="1: requests in needed-at chunks with batch-chain segments overlapped on a second stream "
+                        "(mirsha_hash_requests_then_batches_device); 0: request kernel, then batch kernel")
+    p.add_argument("--events-in-timed-loop", type=int, default=1,
+                   help="1: per-kernel HIP events inside the timed loop (roofline from the same region); "
+                        "0: time the loop bare, then measure kernels in a second identical pass")
     return p.parse_args()
 
 
@@ -150,7 +156,13 @@ def main():
     eng.synth_requests_device(SEED_BASE + a.config, first_req, n, data_len, d_arena.data_ptr())
     torch.cuda.synchronize(dev)
 
+    plan = eng.pipeline(n, idx, first, np.full(n, stride)) if a.pipeline else None
+
     def step():
+        if plan is not None:
+            eng.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
+                                                  d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
+            return
         eng.hash_batch_device(d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr(), None, n,
                               d_req.data_ptr())
         eng.digest_lists_device(d_req.data_ptr(), n, d_idx.data_ptr(), d_first.data_ptr(), nbat, int(first[-1]),
@@ -160,21 +172,30 @@ def main():
         step()
     torch.cuda.synchronize(dev)
 
-    eng.set_timing(True)
-    eng.reset_timing()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    eng.set_timing(False)
+    def timed(with_events):
+        eng.set_timing(with_events)
+        eng.reset_timing()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        eng.set_timing(False)
+        return el
+
+    dt = timed(bool(a.events_in_timed_loop))
+    dt_bare = None
+    if not a.events_in_timed_loop:
+        dt_bare = dt
+        timed(True)
     n_msgs, ms_msgs = eng.kernel_time(KERNEL_MSGS)
     n_lists, ms_lists = eng.kernel_time(KERNEL_LISTS)
+    n_chain, ms_chain = eng.kernel_time(KERNEL_CHAIN)
 
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -202,9 +223,10 @@ def main():
     gbps = bytes_hashed * world * a.steps / dt / 1e9
 
     avg_msgs_ms = ms_msgs / max(n_msgs, 1)
-    avg_lists_ms = ms_lists / max(n_lists, 1)
-    achieved_tops = req_blocks * OPS_PER_COMPRESSION / (avg_msgs_ms * 1e-3) / 1e12
-    hbm_gbs = (n * stride + n * 32) / (avg_msgs_ms * 1e-3) / 1e9
+    msgs_ms_per_step = ms_msgs / a.steps  # all request-chunk launches of one step
+    avg_lists_ms = (ms_lists + ms_chain) / a.steps  # dependent pass device time per step
+    achieved_tops = req_blocks * OPS_PER_COMPRESSION / (msgs_ms_per_step * 1e-3) / 1e12
+    hbm_gbs = (n * stride + n * 32) / (msgs_ms_per_step * 1e-3) / 1e9
 
     traffic = None
     if os.path.exists(a.traffic_file):
@@ -255,7 +277,8 @@ def main():
                 "batch_digests_per_gpu": nbat,
                 "compressions_per_step_per_gpu": req_blocks + bat_blocks,
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": "lds" if a.variant == 0 else "direct",
+                "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx"][a.variant],
+                "pipeline": bool(a.pipeline),
             },
             "gb_per_s_hashed": gbps,
             "roofline": {
@@ -267,12 +290,18 @@ def main():
                 "traffic": traffic,
                 "kernel": "sha256_msgs_kernel",
                 "avg_launch_ms": avg_msgs_ms,
-                "work": f"{req_blocks} compressions x {OPS_PER_COMPRESSION} int32 ops per launch",
+                "launches_per_step": n_msgs / a.steps,
+                "kernel_ms_per_step": msgs_ms_per_step,
+                "work": f"{req_blocks} compressions x {OPS_PER_COMPRESSION} int32 ops per step "
+                        f"(over {n_msgs // a.steps} launch(es))",
                 "hbm_algorithmic_gb_per_s": hbm_gbs,
                 "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
                 "note": "SHA-256 is int32 VALU work (no MFMA shape); hbm/mfma bounds do not apply",
             },
             "batch_kernel_avg_ms": avg_lists_ms,
+            "batch_pass": ("pipelined chain segments %s on a second stream" % (plan.segments() if plan else None))
+                          if plan else "sequential batch kernel",
+            "events_in_timed_loop": bool(a.events_in_timed_loop),
             "self_check": check_ok,
             "pcie_inclusive": pcie,
             "cpu_baseline": cpu,

@@ -78,7 +78,8 @@ void* mirsha_ctx_stream(mirsha_ctx* ctx);
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
 /* Per-kernel device-time accounting with HIP events on the launch stream.
- * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator. */
+ * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator,
+ * 3 = pipelined batch-chain segments (on the context's second stream). */
 int mirsha_ctx_set_timing(mirsha_ctx* ctx, int enable);
 int mirsha_ctx_kernel_time(mirsha_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int mirsha_ctx_reset_timing(mirsha_ctx* ctx);
@@ -140,6 +141,29 @@ int mirsha_hash_batch_device(mirsha_ctx* ctx, const uint8_t* d_arena, uint64_t a
 int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, uint32_t n_digests,
                                const uint32_t* d_idx, const uint32_t* d_list_first, uint32_t n_lists,
                                uint32_t n_entries, uint8_t* d_digests_out);
+
+/* -------------------------------------------- request -> batch pipeline */
+/* The batch digests of a Ready() cycle form sequential SHA chains over the
+ * request digests (batch b = SHA-256(d_0 || ... || d_{n-1}), sequence.go:154-157).
+ * A pipeline plan hashes the requests in chunks ordered by the position at
+ * which a batch first needs them and advances every batch chain segment by
+ * segment on a second stream (midstate carried on device), so the dependent
+ * pass overlaps the request pass instead of following it.  The plan is built
+ * once from the (host) index lists and reused for every run with the same
+ * shape; mirsha_hash_requests_then_batches uses one internally.
+ * len (may be NULL) = request lengths, for bucketing and the cost model. */
+typedef struct mirsha_pipeline mirsha_pipeline;
+int mirsha_pipeline_create(mirsha_ctx* ctx, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
+                           const uint32_t* list_first, uint32_t n_lists, mirsha_pipeline** out);
+void mirsha_pipeline_destroy(mirsha_pipeline* p);
+/* Number of chain segments; bounds (optional, cap entries) = first ordinal of each. */
+int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap);
+/* Device-resident run: request digests to d_req_out (origin order), batch
+ * digests to d_batch_out; asynchronous on the context stream (which is made to
+ * wait for the chain stream before returning). */
+int mirsha_hash_requests_then_batches_device(mirsha_ctx* ctx, mirsha_pipeline* p, const uint8_t* d_arena,
+                                             uint64_t arena_len, const uint64_t* d_off, const uint32_t* d_len,
+                                             uint8_t* d_req_out, uint8_t* d_batch_out);
 
 /* Host helper: order[] = message indices sorted by SHA-256 block count,
  * longest first (stable), so a wave's 64 lanes run equal-length chains.

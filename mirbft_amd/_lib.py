@@ -63,6 +63,13 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint32, c_uint32, c_void_p],
     ),
     "mirsha_bucket_order": (c_int, [c_void_p, c_uint32, c_void_p]),
+    "mirsha_pipeline_create": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32, POINTER(c_void_p)]),
+    "mirsha_pipeline_destroy": (None, [c_void_p]),
+    "mirsha_pipeline_segments": (c_int, [c_void_p, _u32p, c_void_p, c_uint32]),
+    "mirsha_hash_requests_then_batches_device": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "mirsha_hash_batch_multi": (
         c_int,
         [c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p],

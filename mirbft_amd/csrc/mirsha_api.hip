@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -82,7 +83,21 @@ struct mirsha_ctx {
     std::string err;
     DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
     PinnedBuf h_stage;
-    KernelTimer timers[3];
+    KernelTimer timers[4];         // msgs, lists, gen, chain
+    hipStream_t chain_stream = nullptr;  // dependent-pass stream of the pipeline (lazy)
+};
+
+// A request -> batch-digest pipeline plan (see mirsha.h, mirsha_pipeline_create).
+struct mirsha_pipeline {
+    int device = 0;
+    uint32_t n_req = 0, n_lists = 0, n_entries = 0;
+    std::vector<uint32_t> cidx, cfirst;      // compacted lists (no null entries)
+    std::vector<uint32_t> order;             // request processing order
+    std::vector<uint32_t> chunk_begin;       // per chunk: first position in `order`; size n_chunks + 1
+    std::vector<uint32_t> seg_bound;         // segment s covers ordinals [seg_bound[s], seg_bound[s+1])
+    std::vector<hipEvent_t> chunk_done;      // one per chain segment
+    hipEvent_t chain_done = nullptr;
+    DevBuf d_cidx, d_cfirst, d_order, d_state;
 };
 
 namespace {
@@ -118,20 +133,25 @@ hipEvent_t take_event(KernelTimer& t) {
 
 // Brackets one launch with events on the launch stream when timing is on.
 template <class F>
-int timed_launch(mirsha_ctx* c, int which, F&& launch) {
+int timed_launch_on(mirsha_ctx* c, int which, hipStream_t st, F&& launch) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
         e0 = take_event(c->timers[which]);
         e1 = take_event(c->timers[which]);
-        if (e0) (void)hipEventRecord(e0, c->stream);
+        if (e0) (void)hipEventRecord(e0, st);
     }
     hipError_t e = launch();
     if (e != hipSuccess) return fail(c, MIRSHA_EHIP, "kernel launch: %s", hipGetErrorString(e));
     if (c->timing && e0 && e1) {
-        (void)hipEventRecord(e1, c->stream);
+        (void)hipEventRecord(e1, st);
         c->timers[which].pending.emplace_back(e0, e1);
     }
     return MIRSHA_OK;
+}
+
+template <class F>
+int timed_launch(mirsha_ctx* c, int which, F&& launch) {
+    return timed_launch_on(c, which, c->stream, launch);
 }
 
 int use_device(mirsha_ctx* c) {
@@ -286,6 +306,182 @@ int lists_resident(mirsha_ctx* c, const uint8_t* d_digests, uint32_t n_digests, 
     });
 }
 
+// ---- request -> batch-digest pipeline ------------------------------------
+//
+// The dependent pass (batch / VerifyBatch digests over request digests,
+// sequence.go:154-157, batch_tracker.go:147-150) is a set of sequential SHA
+// chains: list k's block b needs only digests 2b and 2b+1.  Requests are
+// therefore hashed in "needed-at" order (their smallest ordinal in any list)
+// in chunks, and each chunk is followed — on a second stream — by one chain
+// SEGMENT that advances every list over the ordinals that chunk completed
+// (midstate carried in d_state).  Segment s runs beside request chunk s+1;
+// only the last segment (<= 2 compressions when the chain is short) is exposed.
+
+constexpr double kChainSecondsPerCompression = 3.0e-6;  // chain wave beside request waves
+constexpr double kRequestCompressionsPerSecond = 21.0e9;
+
+// Measured on MI355X (profiles/r01/pipeline_timeline.txt): a cross-stream
+// event hand-off costs ~17 us per chunk boundary, small request chunks are
+// latency-bound (a wave's own chain), and chain segments overlapped with 8
+// request waves per SIMD slow down ~4x despite s_setprio.  Stream-level
+// pipelining therefore loses at BASELINE sizes; the default plan is ONE
+// segment (request pass, then the chain pass).  MIRSHA_PIPELINE_SEGMENTS=auto
+// enables the cost-model split below for experiments.
+std::vector<uint32_t> plan_segments(uint32_t maxc, double request_seconds) {
+    std::vector<uint32_t> b{0};
+    const char* mode = getenv("MIRSHA_PIPELINE_SEGMENTS");
+    if (!mode || strcmp(mode, "auto") != 0) return b;
+    if (maxc <= 2) return b;
+    const uint32_t top = maxc & ~1u;  // last even ordinal <= maxc
+    const double r = request_seconds / maxc;                // request time per ordinal
+    const double h = kChainSecondsPerCompression / 2.0;     // chain time per ordinal
+    if (h * 2.0 < r) {
+        // Chain much faster than requests: widths grow backwards from a
+        // 2-ordinal tail so that each segment hides behind the next chunk.
+        std::vector<uint32_t> w{2};
+        uint32_t sum = 2;
+        while (sum < top && w.size() < 3) {
+            uint32_t nw = (uint32_t)(w.back() * r / h) & ~1u;
+            if (nw < 2) nw = 2;
+            if (sum + nw > top || w.size() == 2) nw = top - sum;  // first segment takes the rest
+            w.push_back(nw);
+            sum += nw;
+        }
+        uint32_t acc = 0;
+        for (size_t i = w.size(); i-- > 1;) {
+            acc += w[i];
+            b.push_back(acc);
+        }
+    } else {
+        // Chain-bound: start the chain early (small first chunk), then equal segments.
+        const uint32_t S = std::min<uint32_t>(8, top / 2);
+        uint32_t first = ((top / (2 * S)) + 1) & ~1u;
+        if (first < 2) first = 2;
+        b.push_back(first);
+        const uint32_t rest = top - first;
+        for (uint32_t s = 1; s < S && rest; s++) {
+            const uint32_t v = (first + (uint32_t)((uint64_t)rest * s / (S - 1))) & ~1u;
+            if (v > b.back() && v < top) b.push_back(v);
+        }
+    }
+    return b;
+}
+
+int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t* idx, const uint32_t* first,
+                   uint32_t n_lists, const uint32_t* len) {
+    p->n_req = n_req;
+    p->n_lists = n_lists;
+    p->cfirst.assign(n_lists + 1, 0);
+    p->cidx.clear();
+    p->cidx.reserve(first[n_lists]);
+    std::vector<uint32_t> needed(n_req, UINT32_MAX);
+    uint32_t maxc = 0;
+    for (uint32_t k = 0; k < n_lists; k++) {
+        uint32_t ord = 0;
+        for (uint32_t e = first[k]; e < first[k + 1]; e++) {
+            if (idx[e] == MIRSHA_NULL_INDEX) continue;  // empty digest: contributes no bytes
+            p->cidx.push_back(idx[e]);
+            needed[idx[e]] = std::min(needed[idx[e]], ord);
+            ord++;
+        }
+        p->cfirst[k + 1] = (uint32_t)p->cidx.size();
+        maxc = std::max(maxc, ord);
+    }
+    p->n_entries = (uint32_t)p->cidx.size();
+    double comps = 0;
+    for (uint32_t i = 0; i < n_req; i++) comps += len ? host_blocks(len[i]) : 5.0;
+    p->seg_bound = plan_segments(maxc, comps / kRequestCompressionsPerSecond);
+    const uint32_t S = (uint32_t)p->seg_bound.size();
+    // chunk id: segment whose ordinal range holds needed-at; unlisted last (S)
+    auto chunk_of = [&](uint32_t r) -> uint32_t {
+        const uint32_t n = needed[r];
+        if (n == UINT32_MAX) return S;
+        uint32_t s = (uint32_t)(std::upper_bound(p->seg_bound.begin(), p->seg_bound.end(), n) - p->seg_bound.begin()) - 1;
+        return s;
+    };
+    std::vector<uint32_t> cid(n_req);
+    std::vector<uint32_t> cnt(S + 2, 0);
+    for (uint32_t r = 0; r < n_req; r++) {
+        cid[r] = chunk_of(r);
+        cnt[cid[r] + 1]++;
+    }
+    p->chunk_begin.assign(S + 2, 0);
+    for (uint32_t s = 0; s <= S; s++) p->chunk_begin[s + 1] = p->chunk_begin[s] + cnt[s + 1];
+    p->order.assign(n_req, 0);
+    std::vector<uint32_t> pos(p->chunk_begin.begin(), p->chunk_begin.end() - 1);
+    // stable by chunk; within a chunk longest-first by block count (length bucketing)
+    std::vector<uint32_t> byc(n_req);
+    for (uint32_t r = 0; r < n_req; r++) byc[pos[cid[r]]++] = r;
+    if (len) {
+        for (uint32_t s = 0; s <= S; s++) {
+            auto b = byc.begin() + p->chunk_begin[s], e = byc.begin() + p->chunk_begin[s + 1];
+            std::stable_sort(b, e, [&](uint32_t x, uint32_t y) { return host_blocks(len[x]) > host_blocks(len[y]); });
+        }
+    }
+    p->order = std::move(byc);
+    // device copies
+    HIP_TRY(c, p->d_cidx.ensure(sizeof(uint32_t) * std::max<uint32_t>(p->n_entries, 1)));
+    HIP_TRY(c, p->d_cfirst.ensure(sizeof(uint32_t) * (n_lists + 1)));
+    HIP_TRY(c, p->d_order.ensure(sizeof(uint32_t) * std::max<uint32_t>(n_req, 1)));
+    HIP_TRY(c, p->d_state.ensure(32ull * std::max<uint32_t>(n_lists, 1)));
+    if (p->n_entries)
+        HIP_TRY(c, hipMemcpy(p->d_cidx.p, p->cidx.data(), sizeof(uint32_t) * p->n_entries, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(p->d_cfirst.p, p->cfirst.data(), sizeof(uint32_t) * (n_lists + 1), hipMemcpyHostToDevice));
+    if (n_req)
+        HIP_TRY(c, hipMemcpy(p->d_order.p, p->order.data(), sizeof(uint32_t) * n_req, hipMemcpyHostToDevice));
+    p->chunk_done.resize(S, nullptr);
+    for (auto& e : p->chunk_done)
+        if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!p->chain_done) HIP_TRY(c, hipEventCreateWithFlags(&p->chain_done, hipEventDisableTiming));
+    return MIRSHA_OK;
+}
+
+int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
+                 const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
+    if (!c->chain_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->chain_stream, hipStreamNonBlocking));
+    const uint32_t S = (uint32_t)p->seg_bound.size();
+    const uint32_t* order = p->d_order.as<uint32_t>();
+    // The chain stream must not start a new run before the caller's stream
+    // reached it (previous consumers of d_req_out/d_list_out on that stream).
+    HIP_TRY(c, hipEventRecord(p->chain_done, c->stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->chain_stream, p->chain_done, 0));
+    for (uint32_t s = 0; s <= S; s++) {
+        const uint32_t b = p->chunk_begin[s], n = p->chunk_begin[s + 1] - b;
+        if (n) {
+            if (int rc = timed_launch(c, 0, [&] {
+                    return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, d_off, d_len, order + b, n, d_req_out,
+                                               c->variant, c->stream);
+                }))
+                return rc;
+        }
+        if (s == S) break;  // unlisted requests: no chain segment depends on them
+        HIP_TRY(c, hipEventRecord(p->chunk_done[s], c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->chain_stream, p->chunk_done[s], 0));
+        const uint32_t ob = p->seg_bound[s];
+        const uint32_t oe = s + 1 < S ? p->seg_bound[s + 1] : mirsha::kOpenEnd;
+        if (int rc = timed_launch_on(c, 3, c->chain_stream, [&] {
+                return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
+                                            p->d_cfirst.as<uint32_t>(), p->n_lists, ob, oe,
+                                            p->d_state.as<uint32_t>(), d_list_out, c->chain_stream);
+            }))
+            return rc;
+    }
+    // Join: the caller's stream waits for the last chain segment.
+    HIP_TRY(c, hipEventRecord(p->chain_done, c->chain_stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, p->chain_done, 0));
+    return MIRSHA_OK;
+}
+
+void pipeline_free(mirsha_pipeline* p) {
+    for (auto e : p->chunk_done)
+        if (e) (void)hipEventDestroy(e);
+    if (p->chain_done) (void)hipEventDestroy(p->chain_done);
+    p->d_cidx.release();
+    p->d_cfirst.release();
+    p->d_order.release();
+    p->d_state.release();
+}
+
 }  // namespace
 
 extern "C" {
@@ -337,6 +533,7 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     c->d_arena.release(); c->d_off.release(); c->d_len.release(); c->d_order.release();
     c->d_out.release(); c->d_idx.release(); c->d_first.release(); c->d_out2.release(); c->d_scratch.release();
     c->h_stage.release();
+    if (c->chain_stream) (void)hipStreamDestroy(c->chain_stream);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -364,7 +561,7 @@ int mirsha_ctx_set_timing(mirsha_ctx* c, int enable) {
 }
 
 int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double* total_ms) {
-    if (!c || which < 0 || which > 2) return MIRSHA_EINVAL;
+    if (!c || which < 0 || which > 3) return MIRSHA_EINVAL;
     if (int rc = use_device(c)) return rc;
     KernelTimer& t = c->timers[which];
     for (auto& pr : t.pending) {
@@ -384,7 +581,7 @@ int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double*
 
 int mirsha_ctx_reset_timing(mirsha_ctx* c) {
     if (!c) return MIRSHA_EINVAL;
-    for (int k = 0; k < 3; k++) {
+    for (int k = 0; k < 4; k++) {
         int rc = mirsha_ctx_kernel_time(c, k, nullptr, nullptr);
         if (rc) return rc;
         c->timers[k].launches = 0;
@@ -480,6 +677,44 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
         if (int rc = check_lists(c, idx, first, n_batches, n_req)) return rc;
     if (int rc = use_device(c)) return rc;
     HIP_TRY(c, c->d_out.ensure(32ull * std::max<uint32_t>(n_req, 1)));
+    // Dense arena that fits one launch: the pipelined path (requests in
+    // needed-at chunks, batch chains advancing beside them).
+    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
+    for (uint32_t i = 0; i < n_req; i++) {
+        if (len[i] > MIRSHA_MAX_MESSAGE_BYTES) return fail(c, MIRSHA_ERANGE, "message %u too long", i);
+        if (off[i] > arena_len || len[i] > arena_len - off[i]) return fail(c, MIRSHA_EINVAL, "message %u outside arena", i);
+        lo = std::min<uint64_t>(lo, off[i]);
+        hi = std::max<uint64_t>(hi, off[i] + len[i]);
+        total += len[i];
+    }
+    const uint64_t span = n_req ? hi - lo : 0;
+    if (n_batches && n_req && span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES && span <= 2 * total + 4096) {
+        mirsha_pipeline p;
+        p.device = c->device;
+        int rc = pipeline_build(c, &p, n_req, idx, first, n_batches, len);
+        if (rc == MIRSHA_OK) {
+            std::vector<uint64_t> roff(off, off + n_req);
+            for (auto& x : roff) x -= lo;
+            HIP_TRY(c, c->d_arena.ensure(span + kArenaSlack));
+            HIP_TRY(c, c->d_off.ensure(sizeof(uint64_t) * n_req));
+            HIP_TRY(c, c->d_len.ensure(sizeof(uint32_t) * n_req));
+            HIP_TRY(c, c->d_out2.ensure(32ull * n_batches));
+            if (span) HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, arena + lo, span, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(c->d_off.p, roff.data(), sizeof(uint64_t) * n_req, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(c->d_len.p, len, sizeof(uint32_t) * n_req, hipMemcpyHostToDevice, c->stream));
+            rc = pipeline_run(c, &p, c->d_arena.as<uint8_t>(), span, c->d_off.as<uint64_t>(), c->d_len.as<uint32_t>(),
+                              c->d_out.as<uint8_t>(), c->d_out2.as<uint8_t>());
+            if (rc == MIRSHA_OK) {
+                HIP_TRY(c, hipMemcpyAsync(batch_out, c->d_out2.p, 32ull * n_batches, hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipMemcpyAsync(req_out, c->d_out.p, 32ull * n_req, hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));
+            }
+        }
+        (void)hipStreamSynchronize(c->stream);
+        pipeline_free(&p);
+        return rc;
+    }
+    // General path (sparse or windowed arena): all requests, then all lists.
     if (int rc = hash_host_messages(c, arena, arena_len, off, len, n_req, c->d_out.as<uint8_t>())) return rc;
     if (n_batches) {
         HIP_TRY(c, c->d_out2.ensure(32ull * n_batches));
@@ -490,6 +725,51 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
     if (n_req) HIP_TRY(c, hipMemcpyAsync(req_out, c->d_out.p, 32ull * n_req, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return MIRSHA_OK;
+}
+
+int mirsha_pipeline_create(mirsha_ctx* c, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
+                           const uint32_t* list_first, uint32_t n_lists, mirsha_pipeline** out) {
+    if (!c || !out) return MIRSHA_EINVAL;
+    *out = nullptr;
+    if (int rc = check_lists(c, idx, list_first, n_lists, n_req)) return rc;
+    if (int rc = use_device(c)) return rc;
+    mirsha_pipeline* p = new mirsha_pipeline();
+    p->device = c->device;
+    int rc = pipeline_build(c, p, n_req, idx, list_first, n_lists, len);
+    if (rc != MIRSHA_OK) {
+        pipeline_free(p);
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return MIRSHA_OK;
+}
+
+void mirsha_pipeline_destroy(mirsha_pipeline* p) {
+    if (!p) return;
+    (void)hipSetDevice(p->device);
+    pipeline_free(p);
+    delete p;
+}
+
+int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap) {
+    if (!p || !n_segments) return MIRSHA_EINVAL;
+    *n_segments = (uint32_t)p->seg_bound.size();
+    if (bounds)
+        for (uint32_t i = 0; i < cap && i < p->seg_bound.size(); i++) bounds[i] = p->seg_bound[i];
+    return MIRSHA_OK;
+}
+
+int mirsha_hash_requests_then_batches_device(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena,
+                                             uint64_t arena_len, const uint64_t* d_off, const uint32_t* d_len,
+                                             uint8_t* d_req_out, uint8_t* d_batch_out) {
+    if (!c || !p) return MIRSHA_EINVAL;
+    if (p->device != c->device) return fail(c, MIRSHA_EINVAL, "pipeline built for device %d", p->device);
+    if (p->n_req && (!d_off || !d_len || !d_req_out || (!d_arena && arena_len))) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (p->n_lists && !d_batch_out) return fail(c, MIRSHA_EINVAL, "NULL batch output");
+    if (arena_len > MIRSHA_MAX_DEVICE_ARENA_BYTES) return fail(c, MIRSHA_ERANGE, "device arena too large");
+    if (int rc = use_device(c)) return rc;
+    return pipeline_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_batch_out);
 }
 
 int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digests, const uint32_t* idx,

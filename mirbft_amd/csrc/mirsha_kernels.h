@@ -23,6 +23,11 @@ constexpr uint32_t kMaxListDigests = (1u << 27) - 1u;
 constexpr uint32_t kMaxListEntries = (1u << 30) - 1u;
 hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32_t* idx, uint32_t n_entries,
                         const uint32_t* first, uint32_t n_lists, uint32_t* scratch, uint8_t* out, hipStream_t s);
+// One segment [ob, oe) of every (compacted) list chain; oe = kOpenEnd finalises all.
+constexpr uint32_t kOpenEnd = 0xFFFFFFFEu;
+hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
+                        const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
+                        uint8_t* out, hipStream_t s);
 hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
                                uint8_t* arena, hipStream_t s);
 

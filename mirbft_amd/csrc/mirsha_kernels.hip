@@ -315,6 +315,94 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
     if (valid) store_digest(out, k, st);
 }
 
+// Pipelined dependent pass: one SEGMENT of every list's chain.  Lists are
+// compacted (no null entries).  Segment [ob, oe) hashes the full 2-digest
+// blocks of digest ordinals ob .. min(oe, c) (ob, oe even) starting from the
+// midstate in `state` (H0 when ob == 0); a list whose last digest falls in
+// the segment (c <= oe) is finalised (partial block + FIPS padding) and its
+// digest written to out, otherwise the midstate is written back.  Lists with
+// c <= ob (ob > 0) were finalised by an earlier segment and are skipped.
+// The waves raise their issue priority: they run beside the next request
+// chunk and must keep near-alone speed on their SIMD.
+__global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
+    const uint8_t* __restrict__ digests, uint32_t n_digests, const uint32_t* __restrict__ cidx,
+    uint32_t n_entries, const uint32_t* __restrict__ cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe,
+    uint32_t* __restrict__ state, uint8_t* __restrict__ out) {
+    __builtin_amdgcn_s_setprio(3);
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)cidx, (short)0, (int)(4u * n_entries), 0x00020000);
+    const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
+    const bool valid = k < n_lists;
+    const uint32_t e0 = valid ? cfirst[k] : 0u;
+    const uint32_t c = valid ? cfirst[k + 1] - e0 : 0u;
+    const bool active = valid && (ob == 0u || c > ob);
+    const bool fin = active && c <= oe;
+    const uint32_t full_end = fin ? (c & ~1u) : oe;  // exclusive ordinal of the full blocks
+    const uint32_t nblk = active ? (full_end - ob) / 2u + (fin ? 1u : 0u) : 0u;
+    const uint32_t wave_nb = wave_max(nblk);
+    const uint32_t L = 32u * c;
+
+    uint32_t st[8];
+    if (ob == 0u || !active) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    } else {
+        const uint4* sp = reinterpret_cast<const uint4*>(state + 8ull * k);
+        const uint4 s0 = sp[0], s1 = sp[1];
+        st[0] = s0.x; st[1] = s0.y; st[2] = s0.z; st[3] = s0.w;
+        st[4] = s1.x; st[5] = s1.y; st[6] = s1.z; st[7] = s1.w;
+    }
+
+    // Same prefetch pipeline as hash_list: digests one block ahead, indices two.
+    auto live = [&](uint32_t t, uint32_t slot) { return t < nblk && ob + 2u * t + slot < c; };
+    uint4 cur[4];
+    uint32_t nx0 = ld_u32(irs, 4u * (e0 + ob + 2u), live(1, 0)), nx1 = ld_u32(irs, 4u * (e0 + ob + 3u), live(1, 1));
+    {
+        const uint32_t i0 = ld_u32(irs, 4u * (e0 + ob), live(0, 0));
+        const uint32_t i1 = ld_u32(irs, 4u * (e0 + ob + 1u), live(0, 1));
+        load_digest(drs, i0, live(0, 0), cur[0], cur[1]);
+        load_digest(drs, i1, live(0, 1), cur[2], cur[3]);
+    }
+    for (uint32_t t = 0; t < wave_nb; t++) {
+        uint4 nxt[4];
+        load_digest(drs, nx0, live(t + 1, 0), nxt[0], nxt[1]);
+        load_digest(drs, nx1, live(t + 1, 1), nxt[2], nxt[3]);
+        const uint32_t nn0 = ld_u32(irs, 4u * (e0 + ob + 2u * t + 4u), live(t + 2, 0));
+        const uint32_t nn1 = ld_u32(irs, 4u * (e0 + ob + 2u * t + 5u), live(t + 2, 1));
+        if (t < nblk) {
+            uint32_t w[16];
+#pragma unroll
+            for (int half = 0; half < 2; half++) {
+                const uint32_t di = ob + 2u * t + (uint32_t)half;
+                const uint4 x0 = cur[2 * half], x1 = cur[2 * half + 1];
+                w[8 * half + 0] = __builtin_bswap32(x0.x) | (fin && di == c ? 0x80000000u : 0u);
+                w[8 * half + 1] = __builtin_bswap32(x0.y); w[8 * half + 2] = __builtin_bswap32(x0.z);
+                w[8 * half + 3] = __builtin_bswap32(x0.w); w[8 * half + 4] = __builtin_bswap32(x1.x);
+                w[8 * half + 5] = __builtin_bswap32(x1.y); w[8 * half + 6] = __builtin_bswap32(x1.z);
+                w[8 * half + 7] = __builtin_bswap32(x1.w);
+            }
+            if (fin && t + 1u == nblk) {
+                w[14] = L >> 29;
+                w[15] = L << 3;
+            }
+            compress_asm(st, w);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+        nx0 = nn0;
+        nx1 = nn1;
+    }
+    if (fin) {
+        store_digest(out, k, st);
+    } else if (active) {
+        uint4* sp = reinterpret_cast<uint4*>(state + 8ull * k);
+        sp[0] = make_uint4(st[0], st[1], st[2], st[3]);
+        sp[1] = make_uint4(st[4], st[5], st[6], st[7]);
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -376,6 +464,16 @@ hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32
     const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
     sha256_lists_kernel<<<grid, kBlockThreads, 0, s>>>(digests, n_digests, idx, n_entries, first, n_lists, scratch,
                                                       out);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
+                        const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
+                        uint8_t* out, hipStream_t s) {
+    if (n_lists == 0) return hipSuccess;
+    const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
+    sha256_chain_kernel<<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists, ob, oe,
+                                                      state, out);
     return hipGetLastError();
 }
 

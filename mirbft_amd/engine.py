@@ -18,6 +18,7 @@ from ._lib import MIRSHA_NULL_INDEX, MirshaError, check
 KERNEL_MSGS = 0
 KERNEL_LISTS = 1
 KERNEL_GEN = 2
+KERNEL_CHAIN = 3
 VARIANT_LDS = 0
 VARIANT_DIRECT = 1
 VARIANT_LDS_CXX = 2
@@ -191,8 +192,53 @@ class Engine:
         self._check(self._lib.mirsha_digest_lists_device(self.ctx, d_digests, n_digests, d_idx, d_first, n_lists,
                                                          n_entries, d_out))
 
+    def pipeline(self, n_req: int, idx, list_first, length=None) -> "Pipeline":
+        """Plan for request -> batch-digest runs with this list shape (host index lists)."""
+        return Pipeline(self, n_req, idx, list_first, length)
+
+    def hash_requests_then_batches_device(self, plan: "Pipeline", d_arena: int, arena_len: int, d_off: int,
+                                          d_len: int, d_req_out: int, d_batch_out: int) -> None:
+        self._check(self._lib.mirsha_hash_requests_then_batches_device(
+            self.ctx, plan.handle, d_arena, arena_len, d_off, d_len, d_req_out, d_batch_out))
+
     def synth_requests_device(self, seed: int, first: int, count: int, data_len: int, d_arena: int) -> None:
         self._check(self._lib.mirsha_synth_requests_device(self.ctx, seed, first, count, data_len, d_arena))
+
+
+class Pipeline:
+    """mirsha_pipeline: requests hashed in needed-at chunks, batch chains advanced
+    segment by segment beside them (see include/mirsha.h)."""
+
+    def __init__(self, engine: Engine, n_req: int, idx, list_first, length=None):
+        self._lib = engine._lib
+        self._engine = engine
+        ix = np.ascontiguousarray(idx, dtype=np.uint32)
+        fs = np.ascontiguousarray(list_first, dtype=np.uint32)
+        ln = None if length is None else np.ascontiguousarray(length, dtype=np.uint32)
+        h = ctypes.c_void_p()
+        engine._check(self._lib.mirsha_pipeline_create(engine.ctx, int(n_req), _ptr(ln), _ptr(ix), _ptr(fs),
+                                                       int(fs.size) - 1, ctypes.byref(h)))
+        self.handle = h
+        self.n_req = int(n_req)
+        self.n_lists = int(fs.size) - 1
+
+    def segments(self) -> list[int]:
+        n = ctypes.c_uint32(0)
+        check(self._lib.mirsha_pipeline_segments(self.handle, ctypes.byref(n), None, 0))
+        b = np.zeros(max(n.value, 1), dtype=np.uint32)
+        check(self._lib.mirsha_pipeline_segments(self.handle, ctypes.byref(n), _ptr(b), n.value))
+        return b[: n.value].tolist()
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.mirsha_pipeline_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def bucket_order(length: Sequence[int]) -> tuple[np.ndarray, bool]:
@@ -219,6 +265,7 @@ def hash_batch_multi(devices: Iterable[int], arena, off, length) -> np.ndarray:
 
 __all__ = [
     "Engine",
+    "Pipeline",
     "bucket_order",
     "device_count",
     "hash_batch_multi",
@@ -226,6 +273,7 @@ __all__ = [
     "KERNEL_MSGS",
     "KERNEL_LISTS",
     "KERNEL_GEN",
+    "KERNEL_CHAIN",
     "VARIANT_LDS",
     "VARIANT_DIRECT",
 ]

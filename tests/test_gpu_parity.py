@@ -373,3 +373,79 @@ def test_device_lists_with_nulls_and_empty(engine):
                                int(first[-1]), d_out.data_ptr())
     engine.sync()
     assert np.array_equal(d_out.cpu().numpy(), oracle_py.batch_digests(dig, idx, first))
+
+
+@pytest.mark.parametrize("cfg,data_len,n,bs", [(2, 256, 1 << 20, 20), (3, 4096, 1 << 18, 500), (9, 100, 5003, 7)])
+def test_pipeline_device_full_size(engine, cfg, data_len, n, bs):
+    """Pipelined request -> batch digests (needed-at chunks + chain segments on a
+    second stream) at BASELINE sizes, bit-exact vs the oracle, run twice on the
+    same plan (midstate buffers reused)."""
+    torch = _torch()
+    stride = 16 + data_len
+    seed = synth.SEED_BASE + cfg
+    idx, first = sharding.batch_lists(n, bs)
+    plan = engine.pipeline(n, idx, first, np.full(n, stride))
+    segs = plan.segments()
+    assert segs[0] == 0
+    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    d_req = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
+    arena = oracle_py.gen_requests(seed, 0, n, data_len)
+    want_req = oracle_py.hash_requests(arena, np.arange(n, dtype=np.uint64) * stride, np.full(n, stride), threads=8)
+    want_bat = oracle_py.batch_digests(want_req, idx, first)
+    for _ in range(2):
+        d_req.zero_()
+        d_bat.zero_()
+        engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
+                                                 d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
+        engine.sync()
+        assert np.array_equal(d_req.cpu().numpy(), want_req)
+        assert np.array_equal(d_bat.cpu().numpy(), want_bat)
+    plan.close()
+
+
+def test_pipeline_multi_segment_env(engine, monkeypatch):
+    """The experimental multi-segment split (MIRSHA_PIPELINE_SEGMENTS=auto) stays bit-exact."""
+    monkeypatch.setenv("MIRSHA_PIPELINE_SEGMENTS", "auto")
+    torch = _torch()
+    n, data_len, bs = 40000, 256, 20
+    stride = 16 + data_len
+    idx, first = sharding.batch_lists(n, bs)
+    plan = engine.pipeline(n, idx, first, np.full(n, stride))
+    assert len(plan.segments()) > 1
+    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    d_req = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    engine.synth_requests_device(5, 0, n, data_len, d_arena.data_ptr())
+    engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
+                                             d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
+    engine.sync()
+    want_req = oracle_py.hash_requests(oracle_py.gen_requests(5, 0, n, data_len),
+                                       np.arange(n, dtype=np.uint64) * stride, np.full(n, stride))
+    assert np.array_equal(d_req.cpu().numpy(), want_req)
+    assert np.array_equal(d_bat.cpu().numpy(), oracle_py.batch_digests(want_req, idx, first))
+    plan.close()
+
+
+def test_pipeline_irregular_lists(engine):
+    """Shared requests, unlisted requests, nulls, empty and odd lists through the pipeline."""
+    rng = np.random.default_rng(21)
+    n = 3000
+    lens = rng.integers(0, 600, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(lens[:-1], out=off[1:])
+    arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    sizes = rng.integers(0, 60, 300)
+    sizes[::9] = 0
+    idx = rng.integers(0, n // 2, int(sizes.sum())).astype(np.uint32)  # half the requests unlisted
+    idx[rng.random(idx.size) < 0.1] = _lib.MIRSHA_NULL_INDEX
+    first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    req, bat = engine.hash_requests_then_batches(arena, off, lens, idx, first)
+    want_req = oracle_py.hash_requests(arena, off, lens)
+    assert np.array_equal(req, want_req)
+    assert np.array_equal(bat, oracle_py.batch_digests(want_req, idx, first))
