@@ -53,7 +53,8 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=100,
+                   help="untimed steps; MI355X needs ~20+ ms of sustained load to reach its working clock")
     p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     p.add_argument("--variant", type=int, default=0, help="0 = LDS-staged loader, 1 = direct per-lane loads")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline sample (0 disables)")

@@ -688,7 +688,10 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
         total += len[i];
     }
     const uint64_t span = n_req ? hi - lo : 0;
-    if (n_batches && n_req && span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES && span <= 2 * total + 4096) {
+    const char* seg_mode = getenv("MIRSHA_PIPELINE_SEGMENTS");
+    const bool pipelined = seg_mode && strcmp(seg_mode, "auto") == 0;  // see plan_segments()
+    if (pipelined && n_batches && n_req && span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES &&
+        span <= 2 * total + 4096) {
         mirsha_pipeline p;
         p.device = c->device;
         int rc = pipeline_build(c, &p, n_req, idx, first, n_batches, len);
