@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mirbft_amd import Engine, sharding  # noqa: E402
-from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
+from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
 
 SEED_BASE = 0x6D69726266740000
 # Algorithmic work unit: one 64-byte SHA-256 compression = 1384 int32 VALU ops
@@ -60,9 +60,10 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline sample (0 disables)")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-API measurement")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    p.add_argument("--pipeline", type=int, default=0,
-                   help="1: requests in needed-at chunks with batch-chain segments overlapped on a second stream "
-                        "(mirsha_hash_requests_then_batches_device); 0: request kernel, then batch kernel")
+    p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential", "streams"],
+                   help="auto: mirsha_pipeline plan, AUTO mode (fused launch for long chains, else request "
+                        "kernel then list kernel); none: plain device API (request kernel, then batch kernel); "
+                        "fused / sequential / streams: force a plan mode (A/B)")
     p.add_argument("--events-in-timed-loop", type=int, default=1,
                    help="1: per-kernel HIP events inside the timed loop (roofline from the same region); "
                         "0: time the loop bare, then measure kernels in a second identical pass")
@@ -157,7 +158,7 @@ def main():
     eng.synth_requests_device(SEED_BASE + a.config, first_req, n, data_len, d_arena.data_ptr())
     torch.cuda.synchronize(dev)
 
-    plan = eng.pipeline(n, idx, first, np.full(n, stride)) if a.pipeline else None
+    plan = eng.pipeline(n, idx, first, np.full(n, stride), mode=a.pipeline) if a.pipeline != "none" else None
 
     def step():
         if plan is not None:
@@ -197,6 +198,9 @@ def main():
     n_msgs, ms_msgs = eng.kernel_time(KERNEL_MSGS)
     n_lists, ms_lists = eng.kernel_time(KERNEL_LISTS)
     n_chain, ms_chain = eng.kernel_time(KERNEL_CHAIN)
+    n_fused, ms_fused = eng.kernel_time(KERNEL_FUSED)
+    if plan is not None:
+        plan.status()  # raises if a fused run's readiness watchdog ever expired
 
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -223,11 +227,19 @@ def main():
     value = digests_per_step * world * a.steps / dt
     gbps = bytes_hashed * world * a.steps / dt / 1e9
 
-    avg_msgs_ms = ms_msgs / max(n_msgs, 1)
-    msgs_ms_per_step = ms_msgs / a.steps  # all request-chunk launches of one step
-    avg_lists_ms = (ms_lists + ms_chain) / a.steps  # dependent pass device time per step
-    achieved_tops = req_blocks * OPS_PER_COMPRESSION / (msgs_ms_per_step * 1e-3) / 1e12
-    hbm_gbs = (n * stride + n * 32) / (msgs_ms_per_step * 1e-3) / 1e9
+    fused = n_fused > 0
+    if fused:
+        # One persistent launch does the request AND the batch compressions.
+        kname, n_k, ms_k, work_blocks = "sha256_fused_paced_kernel", n_fused, ms_fused, req_blocks + bat_blocks
+        hbm_bytes = n * stride + n * 32 + int(first[-1]) * 32 + nbat * 32
+    else:
+        kname, n_k, ms_k, work_blocks = "sha256_msgs_kernel", n_msgs, ms_msgs, req_blocks
+        hbm_bytes = n * stride + n * 32
+    avg_msgs_ms = ms_k / max(n_k, 1)
+    msgs_ms_per_step = ms_k / a.steps  # all launches of the dominant kernel in one step
+    avg_lists_ms = (ms_lists + ms_chain) / a.steps  # separate dependent pass device time per step
+    achieved_tops = work_blocks * OPS_PER_COMPRESSION / (msgs_ms_per_step * 1e-3) / 1e12
+    hbm_gbs = hbm_bytes / (msgs_ms_per_step * 1e-3) / 1e9
 
     traffic = None
     if os.path.exists(a.traffic_file):
@@ -279,7 +291,7 @@ def main():
                 "compressions_per_step_per_gpu": req_blocks + bat_blocks,
                 "parallelism": f"request-range shards x{world}, no collective",
                 "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx"][a.variant],
-                "pipeline": bool(a.pipeline),
+                "pipeline": a.pipeline if plan is None else f"{a.pipeline} -> {plan.mode_name}",
             },
             "gb_per_s_hashed": gbps,
             "roofline": {
@@ -289,19 +301,22 @@ def main():
                 "unit": "TOP/s",
                 "frac": achieved_tops / VALU_PEAK_TOPS,
                 "traffic": traffic,
-                "kernel": "sha256_msgs_kernel",
+                "kernel": kname,
                 "avg_launch_ms": avg_msgs_ms,
-                "launches_per_step": n_msgs / a.steps,
+                "launches_per_step": n_k / a.steps,
                 "kernel_ms_per_step": msgs_ms_per_step,
-                "work": f"{req_blocks} compressions x {OPS_PER_COMPRESSION} int32 ops per step "
-                        f"(over {n_msgs // a.steps} launch(es))",
+                "work": f"{work_blocks} compressions x {OPS_PER_COMPRESSION} int32 ops per step "
+                        f"(over {n_k // a.steps} launch(es))",
                 "hbm_algorithmic_gb_per_s": hbm_gbs,
                 "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
                 "note": "SHA-256 is int32 VALU work (no MFMA shape); hbm/mfma bounds do not apply",
             },
             "batch_kernel_avg_ms": avg_lists_ms,
-            "batch_pass": ("pipelined chain segments %s on a second stream" % (plan.segments() if plan else None))
-                          if plan else "sequential batch kernel",
+            "batch_pass": {"none": "sequential batch kernel (plain device API)",
+                           "fused": "fused into the request launch (readiness counters, no second kernel)",
+                           "sequential": "plan: request kernel then batch kernel",
+                           "streams": "chain segments %s on a second stream" % (plan.segments() if plan else None),
+                           }[plan.mode_name if plan is not None else "none"],
             "events_in_timed_loop": bool(a.events_in_timed_loop),
             "self_check": check_ok,
             "pcie_inclusive": pcie,

@@ -79,7 +79,8 @@ int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
 /* Per-kernel device-time accounting with HIP events on the launch stream.
  * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator,
- * 3 = pipelined batch-chain segments (on the context's second stream). */
+ * 3 = pipelined batch-chain segments (on the context's second stream),
+ * 4 = fused request -> batch kernel (one persistent launch per run). */
 int mirsha_ctx_set_timing(mirsha_ctx* ctx, int enable);
 int mirsha_ctx_kernel_time(mirsha_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int mirsha_ctx_reset_timing(mirsha_ctx* ctx);
@@ -145,17 +146,48 @@ int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, uint32
 /* -------------------------------------------- request -> batch pipeline */
 /* The batch digests of a Ready() cycle form sequential SHA chains over the
  * request digests (batch b = SHA-256(d_0 || ... || d_{n-1}), sequence.go:154-157).
- * A pipeline plan hashes the requests in chunks ordered by the position at
- * which a batch first needs them and advances every batch chain segment by
- * segment on a second stream (midstate carried on device), so the dependent
- * pass overlaps the request pass instead of following it.  The plan is built
- * once from the (host) index lists and reused for every run with the same
- * shape; mirsha_hash_requests_then_batches uses one internally.
- * len (may be NULL) = request lengths, for bucketing and the cost model. */
+ * A pipeline plan overlaps the dependent pass with the request pass.  It is
+ * built once from the (host) index lists and reused for every run with the
+ * same shape (device API below); a plan is single-stream, like its context.
+ * len (may be NULL) = request lengths, for length bucketing.
+ *   MIRSHA_PIPELINE_FUSED: ONE launch.  Requests are hashed in the order in
+ *     which the lists first need them, one tile wave per SIMD so tiles finish
+ *     in that order; chain waves, alone on a few CUs, advance each list chunk
+ *     by chunk as device-side readiness counters report the feeding request
+ *     tiles done (no host round trip, no second stream).  Pays for a few long
+ *     chains (VerifyBatch of hundreds of digests).
+ *   MIRSHA_PIPELINE_SEQUENTIAL: request kernel at full occupancy, then the
+ *     list kernel.  Best for many short lists (BatchSize 20).
+ *   MIRSHA_PIPELINE_STREAMS: requests in needed-at chunks with batch-chain
+ *     segments on a second stream (midstate carried on device); measured
+ *     slower at BASELINE sizes, kept for A/B.
+ *   MIRSHA_PIPELINE_AUTO (default): FUSED when the longest list is >= 64
+ *     blocks (~126 digests) and there are <= 64 list groups, else SEQUENTIAL;
+ *     mirsha_pipeline_mode() reports the choice.
+ * mirsha_pipeline_create reads MIRSHA_PIPELINE_MODE (auto | fused |
+ * sequential | streams; default auto). */
+#define MIRSHA_PIPELINE_SEQUENTIAL 0
+#define MIRSHA_PIPELINE_FUSED 1
+#define MIRSHA_PIPELINE_STREAMS 2
+#define MIRSHA_PIPELINE_AUTO 3
 typedef struct mirsha_pipeline mirsha_pipeline;
 int mirsha_pipeline_create(mirsha_ctx* ctx, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
                            const uint32_t* list_first, uint32_t n_lists, mirsha_pipeline** out);
+int mirsha_pipeline_create_mode(mirsha_ctx* ctx, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
+                                const uint32_t* list_first, uint32_t n_lists, int mode, mirsha_pipeline** out);
 void mirsha_pipeline_destroy(mirsha_pipeline* p);
+int mirsha_pipeline_mode(const mirsha_pipeline* p);
+/* Synchronises the context stream and reports a fused run whose readiness
+ * watchdog expired (MIRSHA_EHIP; never expected, the launch is deadlock-free
+ * by construction).  MIRSHA_OK otherwise. */
+int mirsha_pipeline_status(mirsha_ctx* ctx, mirsha_pipeline* p);
+/* Diagnostics of a fused plan created with MIRSHA_FUSED_TRACE=1 in the
+ * environment: the last run's timeline (s_memrealtime ticks, 100 MHz) --
+ * per tile [start, end] at [2t, 2t+1], per readiness chunk the time its list
+ * wave passed the wait at [2 n_tiles + c], per list group its end at
+ * [2 n_tiles + n_counters + g].  *words = total length (0 when tracing is off). */
+int mirsha_pipeline_trace(mirsha_ctx* ctx, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words);
+int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t* n_counters, uint32_t* n_groups);
 /* Number of chain segments; bounds (optional, cap entries) = first ordinal of each. */
 int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap);
 /* Device-resident run: request digests to d_req_out (origin order), batch

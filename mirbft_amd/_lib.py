@@ -64,7 +64,15 @@ SIGNATURES = {
     ),
     "mirsha_bucket_order": (c_int, [c_void_p, c_uint32, c_void_p]),
     "mirsha_pipeline_create": (c_int, [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32, POINTER(c_void_p)]),
+    "mirsha_pipeline_create_mode": (
+        c_int,
+        [c_void_p, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32, c_int, POINTER(c_void_p)],
+    ),
     "mirsha_pipeline_destroy": (None, [c_void_p]),
+    "mirsha_pipeline_mode": (c_int, [c_void_p]),
+    "mirsha_pipeline_status": (c_int, [c_void_p, c_void_p]),
+    "mirsha_pipeline_trace": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "mirsha_pipeline_shape": (c_int, [c_void_p, _u32p, _u32p, _u32p]),
     "mirsha_pipeline_segments": (c_int, [c_void_p, _u32p, c_void_p, c_uint32]),
     "mirsha_hash_requests_then_batches_device": (
         c_int,

@@ -24,6 +24,8 @@ namespace {
 
 constexpr uint64_t kPackWindow = 256ull << 20;  // bytes per packed H2D chunk
 constexpr uint64_t kArenaSlack = 256;           // loader may touch up to 80 B past a message
+constexpr uint32_t kFusedMaxListWaves = 64;      // chain waves of a fused launch (16 CUs)
+constexpr uint32_t kFusedMinChainBlocks = 64;    // AUTO picks the fused launch from this chain length
 
 struct DevBuf {
     void* p = nullptr;
@@ -83,14 +85,23 @@ struct mirsha_ctx {
     std::string err;
     DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
     PinnedBuf h_stage;
-    KernelTimer timers[4];         // msgs, lists, gen, chain
+    KernelTimer timers[5];         // msgs, lists, gen, chain, fused
     hipStream_t chain_stream = nullptr;  // dependent-pass stream of the pipeline (lazy)
 };
 
 // A request -> batch-digest pipeline plan (see mirsha.h, mirsha_pipeline_create).
 struct mirsha_pipeline {
     int device = 0;
+    int mode = MIRSHA_PIPELINE_FUSED;
     uint32_t n_req = 0, n_lists = 0, n_entries = 0;
+    // fused mode (one persistent launch, see mirsha_kernels.hip)
+    std::vector<uint32_t> tadj_first, tadj, cbase, expected;
+    uint32_t n_tiles = 0, n_groups = 0, n_counters = 0, grid = 0;
+    uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
+    uint64_t tile_base = 0, list_base = 0;
+    uint32_t epoch = 0;
+    DevBuf d_tadj_first, d_tadj, d_cbase, d_expected, d_counters, d_ctl, d_trace;
+    bool trace = false;
     std::vector<uint32_t> cidx, cfirst;      // compacted lists (no null entries)
     std::vector<uint32_t> order;             // request processing order
     std::vector<uint32_t> chunk_begin;       // per chunk: first position in `order`; size n_chunks + 1
@@ -327,11 +338,9 @@ constexpr double kRequestCompressionsPerSecond = 21.0e9;
 // pipelining therefore loses at BASELINE sizes; the default plan is ONE
 // segment (request pass, then the chain pass).  MIRSHA_PIPELINE_SEGMENTS=auto
 // enables the cost-model split below for experiments.
-std::vector<uint32_t> plan_segments(uint32_t maxc, double request_seconds) {
+std::vector<uint32_t> plan_segments(uint32_t maxc, double request_seconds, bool split) {
     std::vector<uint32_t> b{0};
-    const char* mode = getenv("MIRSHA_PIPELINE_SEGMENTS");
-    if (!mode || strcmp(mode, "auto") != 0) return b;
-    if (maxc <= 2) return b;
+    if (!split || maxc <= 2) return b;
     const uint32_t top = maxc & ~1u;  // last even ordinal <= maxc
     const double r = request_seconds / maxc;                // request time per ordinal
     const double h = kChainSecondsPerCompression / 2.0;     // chain time per ordinal
@@ -390,7 +399,7 @@ int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint
     p->n_entries = (uint32_t)p->cidx.size();
     double comps = 0;
     for (uint32_t i = 0; i < n_req; i++) comps += len ? host_blocks(len[i]) : 5.0;
-    p->seg_bound = plan_segments(maxc, comps / kRequestCompressionsPerSecond);
+    p->seg_bound = plan_segments(maxc, comps / kRequestCompressionsPerSecond, p->mode == MIRSHA_PIPELINE_STREAMS);
     const uint32_t S = (uint32_t)p->seg_bound.size();
     // chunk id: segment whose ordinal range holds needed-at; unlisted last (S)
     auto chunk_of = [&](uint32_t r) -> uint32_t {
@@ -438,9 +447,25 @@ int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint
 
 int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
                  const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
-    if (!c->chain_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->chain_stream, hipStreamNonBlocking));
     const uint32_t S = (uint32_t)p->seg_bound.size();
     const uint32_t* order = p->d_order.as<uint32_t>();
+    if (S == 1) {
+        // Sequential: request kernel, then the list chains on the same stream.
+        const uint32_t n = p->chunk_begin[S + 1];
+        if (n) {
+            if (int rc = timed_launch(c, 0, [&] {
+                    return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, d_off, d_len, order, n, d_req_out,
+                                               c->variant, c->stream);
+                }))
+                return rc;
+        }
+        return timed_launch(c, 1, [&] {
+            return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
+                                        p->d_cfirst.as<uint32_t>(), p->n_lists, 0u, mirsha::kOpenEnd,
+                                        p->d_state.as<uint32_t>(), d_list_out, c->stream);
+        });
+    }
+    if (!c->chain_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->chain_stream, hipStreamNonBlocking));
     // The chain stream must not start a new run before the caller's stream
     // reached it (previous consumers of d_req_out/d_list_out on that stream).
     HIP_TRY(c, hipEventRecord(p->chain_done, c->stream));
@@ -472,6 +497,203 @@ int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint
     return MIRSHA_OK;
 }
 
+
+// ---- fused plan: one launch (sha256_fused_paced_kernel) ----------------------
+//
+// Host work per plan (once per shape): compacted lists, needed-at processing
+// order, and for every (tile, list-group chunk) pair that feeds it one
+// readiness counter increment; expected[ctr] = number of distinct feeding tiles.
+int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t* idx, const uint32_t* first,
+                uint32_t n_lists, const uint32_t* len) {
+    p->n_req = n_req;
+    p->n_lists = n_lists;
+    p->cfirst.assign(n_lists + 1, 0);
+    p->cidx.clear();
+    p->cidx.reserve(first[n_lists]);
+    std::vector<uint32_t> needed(n_req, UINT32_MAX);
+    for (uint32_t k = 0; k < n_lists; k++) {
+        uint32_t ord = 0;
+        for (uint32_t e = first[k]; e < first[k + 1]; e++) {
+            if (idx[e] == MIRSHA_NULL_INDEX) continue;  // empty digest: contributes no bytes
+            p->cidx.push_back(idx[e]);
+            needed[idx[e]] = std::min(needed[idx[e]], ord);
+            ord++;
+        }
+        p->cfirst[k + 1] = (uint32_t)p->cidx.size();
+    }
+    p->n_entries = (uint32_t)p->cidx.size();
+    if (n_req > (1u << 26)) return fail(c, MIRSHA_ERANGE, "fused plan: %u requests > 2^26", n_req);
+    // Processing order: needed-at ordinal ascending (unlisted last), then
+    // block count descending (length bucketing inside a wave).
+    p->order.resize(n_req);
+    for (uint32_t r = 0; r < n_req; r++) p->order[r] = r;
+    std::stable_sort(p->order.begin(), p->order.end(), [&](uint32_t x, uint32_t y) {
+        if (needed[x] != needed[y]) return needed[x] < needed[y];
+        return len ? host_blocks(len[x]) > host_blocks(len[y]) : false;
+    });
+    std::vector<uint32_t> pos_of(n_req);
+    for (uint32_t i = 0; i < n_req; i++) pos_of[p->order[i]] = i;
+    p->n_tiles = (n_req + 63u) / 64u;
+    p->n_groups = (n_lists + 63u) / 64u;
+    // Counters: group g owns chunks [cbase[g], cbase[g+1]).
+    constexpr uint32_t K = mirsha::kFusedChunkBlocks;
+    p->cbase.assign(p->n_groups + 1, 0);
+    for (uint32_t g = 0; g < p->n_groups; g++) {
+        uint32_t nbmax = 0;
+        for (uint32_t k = 64u * g; k < std::min(n_lists, 64u * g + 64u); k++)
+            nbmax = std::max(nbmax, host_blocks(32u * (p->cfirst[k + 1] - p->cfirst[k])));
+        p->cbase[g + 1] = p->cbase[g] + (nbmax + K - 1u) / K;
+    }
+    p->n_counters = p->cbase[p->n_groups];
+    std::vector<uint64_t> pairs;
+    pairs.reserve(p->n_entries);
+    for (uint32_t k = 0; k < n_lists; k++) {
+        const uint32_t cb = p->cbase[k >> 6];
+        for (uint32_t e = p->cfirst[k]; e < p->cfirst[k + 1]; e++) {
+            const uint32_t o = e - p->cfirst[k];
+            pairs.push_back(((uint64_t)(pos_of[p->cidx[e]] >> 6) << 32) | (cb + (o >> 1) / K));
+        }
+    }
+    std::sort(pairs.begin(), pairs.end());
+    pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
+    p->tadj_first.assign(p->n_tiles + 1, 0);
+    p->tadj.resize(pairs.size());
+    p->expected.assign(std::max<uint32_t>(p->n_counters, 1), 0);
+    for (size_t i = 0; i < pairs.size(); i++) {
+        p->tadj_first[(pairs[i] >> 32) + 1]++;
+        p->tadj[i] = (uint32_t)pairs[i];
+        p->expected[(uint32_t)pairs[i]]++;
+    }
+    for (uint32_t t = 0; t < p->n_tiles; t++) p->tadj_first[t + 1] += p->tadj_first[t];
+    // Grid: one block per CU.  List blocks (4 chain waves each, alone on their
+    // SIMDs: a chain is latency-bound) + tile blocks on the remaining CUs with
+    // ONE tile wave per SIMD, so tiles complete in ticket order generation by
+    // generation and the chains can follow them (measured: two tile waves per
+    // SIMD halve the number of generations and lose, profiles/r01).
+    hipDeviceProp_t prop;
+    HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
+    const uint32_t cus = (uint32_t)prop.multiProcessorCount;
+    p->pace = 1;
+    const uint32_t lw = std::min<uint32_t>(p->n_groups, kFusedMaxListWaves);
+    p->list_blocks = std::min<uint32_t>((lw + 3u) / 4u, cus / 4u);
+    const uint32_t tile_blocks =
+        std::max<uint32_t>(1, std::min<uint32_t>(cus - p->list_blocks, (p->n_tiles + 4u * p->pace - 1u) / (4u * p->pace)));
+    p->tile_waves = tile_blocks * 4u * p->pace;
+    p->grid = p->list_blocks + tile_blocks;
+    // Device copies.
+    auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
+        HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
+        if (bytes) HIP_TRY(c, hipMemcpy(d.p, h, bytes, hipMemcpyHostToDevice));
+        return MIRSHA_OK;
+    };
+    if (int rc = up(p->d_cidx, p->cidx.data(), sizeof(uint32_t) * p->n_entries)) return rc;
+    if (int rc = up(p->d_cfirst, p->cfirst.data(), sizeof(uint32_t) * (n_lists + 1))) return rc;
+    if (int rc = up(p->d_order, p->order.data(), sizeof(uint32_t) * n_req)) return rc;
+    if (int rc = up(p->d_tadj_first, p->tadj_first.data(), sizeof(uint32_t) * (p->n_tiles + 1))) return rc;
+    if (int rc = up(p->d_tadj, p->tadj.data(), sizeof(uint32_t) * p->tadj.size())) return rc;
+    if (int rc = up(p->d_cbase, p->cbase.data(), sizeof(uint32_t) * (p->n_groups + 1))) return rc;
+    if (int rc = up(p->d_expected, p->expected.data(), sizeof(uint32_t) * p->expected.size())) return rc;
+    HIP_TRY(c, p->d_counters.ensure(8ull * std::max<uint32_t>(p->n_counters, 1)));
+    HIP_TRY(c, hipMemset(p->d_counters.p, 0, 8ull * std::max<uint32_t>(p->n_counters, 1)));
+    HIP_TRY(c, p->d_ctl.ensure(8ull * mirsha::kCtlWords));
+    HIP_TRY(c, hipMemset(p->d_ctl.p, 0, 8ull * mirsha::kCtlWords));
+    p->tile_base = p->list_base = 0;
+    p->epoch = 0;
+    const char* tr = getenv("MIRSHA_FUSED_TRACE");
+    p->trace = tr && atoi(tr) != 0;
+    if (p->trace) {
+        const size_t words = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
+        HIP_TRY(c, p->d_trace.ensure(8ull * std::max<size_t>(words, 1)));
+        HIP_TRY(c, hipMemset(p->d_trace.p, 0, 8ull * std::max<size_t>(words, 1)));
+    }
+    return MIRSHA_OK;
+}
+
+int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
+              const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
+    if (p->n_tiles + p->n_groups == 0) return MIRSHA_OK;
+    mirsha::FusedArgs a{};
+    a.arena = d_arena;
+    a.off = d_off;
+    a.len = d_len;
+    a.order = p->d_order.as<uint32_t>();
+    a.req_out = d_req_out;
+    a.cidx = p->d_cidx.as<uint32_t>();
+    a.cfirst = p->d_cfirst.as<uint32_t>();
+    a.list_out = d_list_out;
+    a.tadj_first = p->d_tadj_first.as<uint32_t>();
+    a.tadj = p->d_tadj.as<uint32_t>();
+    a.cbase = p->d_cbase.as<uint32_t>();
+    a.expected = p->d_expected.as<uint32_t>();
+    a.counters = p->d_counters.as<unsigned long long>();
+    a.ctl = p->d_ctl.as<unsigned long long>();
+    a.trace = p->trace ? p->d_trace.as<unsigned long long>() : nullptr;
+    a.n_counters = p->n_counters;
+    a.tile_base = p->tile_base;
+    a.list_base = p->list_base;
+    a.arena_len = (uint32_t)arena_len;
+    a.n_req = p->n_req;
+    a.n_entries = p->n_entries;
+    a.n_lists = p->n_lists;
+    a.epoch = p->epoch + 1u;
+    a.n_tiles = p->n_tiles;
+    a.n_groups = p->n_groups;
+    a.list_waves = p->list_blocks;
+    if (int rc = timed_launch(c, 4, [&] { return mirsha::launch_fused_paced(a, p->grid, p->pace, c->stream); }))
+        return rc;
+    // Tile waves and list waves each made exactly one failing claim on their ticket.
+    p->tile_base += p->n_tiles + p->tile_waves;
+    p->list_base += p->n_groups + (uint64_t)p->list_blocks * 4u;
+    p->epoch++;
+    return MIRSHA_OK;
+}
+
+int fused_status(mirsha_ctx* c, mirsha_pipeline* p) {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (p->mode != MIRSHA_PIPELINE_FUSED || !p->d_ctl.p) return MIRSHA_OK;
+    unsigned long long e = 0;
+    HIP_TRY(c, hipMemcpy(&e, p->d_ctl.as<unsigned long long>() + mirsha::kCtlError, 8, hipMemcpyDeviceToHost));
+    if (e) return fail(c, MIRSHA_EHIP, "fused pass: a list wave's readiness wait expired (watchdog)");
+    return MIRSHA_OK;
+}
+
+// AUTO: the fused launch pays when a few LONG chains would otherwise run after
+// the request pass (VerifyBatch of hundreds of digests, BASELINE config 3:
+// 1.49 -> 1.04 ms); many short lists (BatchSize 20, config 2) run better as
+// the request kernel at full occupancy followed by the list kernel.
+bool fused_pays(const uint32_t* idx, const uint32_t* first, uint32_t n_lists) {
+    if (n_lists == 0 || (n_lists + 63u) / 64u > kFusedMaxListWaves) return false;
+    uint32_t maxc = 0;
+    for (uint32_t k = 0; k < n_lists; k++) {
+        uint32_t c = 0;
+        for (uint32_t e = first[k]; e < first[k + 1]; e++) c += idx[e] != MIRSHA_NULL_INDEX;
+        maxc = std::max(maxc, c);
+    }
+    return host_blocks(32u * maxc) >= kFusedMinChainBlocks;
+}
+
+int plan_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t* idx, const uint32_t* first,
+               uint32_t n_lists, const uint32_t* len) {
+    if (p->mode == MIRSHA_PIPELINE_AUTO)
+        p->mode = fused_pays(idx, first, n_lists) ? MIRSHA_PIPELINE_FUSED : MIRSHA_PIPELINE_SEQUENTIAL;
+    if (p->mode == MIRSHA_PIPELINE_FUSED) return fused_build(c, p, n_req, idx, first, n_lists, len);
+    return pipeline_build(c, p, n_req, idx, first, n_lists, len);
+}
+
+int plan_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
+             const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
+    if (p->mode == MIRSHA_PIPELINE_FUSED) return fused_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
+    return pipeline_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
+}
+
+int default_pipeline_mode() {
+    const char* m = getenv("MIRSHA_PIPELINE_MODE");
+    if (m && strcmp(m, "sequential") == 0) return MIRSHA_PIPELINE_SEQUENTIAL;
+    if (m && strcmp(m, "streams") == 0) return MIRSHA_PIPELINE_STREAMS;
+    if (m && strcmp(m, "fused") == 0) return MIRSHA_PIPELINE_FUSED;
+    return MIRSHA_PIPELINE_AUTO;
+}
+
 void pipeline_free(mirsha_pipeline* p) {
     for (auto e : p->chunk_done)
         if (e) (void)hipEventDestroy(e);
@@ -480,6 +702,13 @@ void pipeline_free(mirsha_pipeline* p) {
     p->d_cfirst.release();
     p->d_order.release();
     p->d_state.release();
+    p->d_tadj_first.release();
+    p->d_tadj.release();
+    p->d_cbase.release();
+    p->d_expected.release();
+    p->d_counters.release();
+    p->d_ctl.release();
+    p->d_trace.release();
 }
 
 }  // namespace
@@ -561,7 +790,7 @@ int mirsha_ctx_set_timing(mirsha_ctx* c, int enable) {
 }
 
 int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double* total_ms) {
-    if (!c || which < 0 || which > 3) return MIRSHA_EINVAL;
+    if (!c || which < 0 || which > 4) return MIRSHA_EINVAL;
     if (int rc = use_device(c)) return rc;
     KernelTimer& t = c->timers[which];
     for (auto& pr : t.pending) {
@@ -581,7 +810,7 @@ int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double*
 
 int mirsha_ctx_reset_timing(mirsha_ctx* c) {
     if (!c) return MIRSHA_EINVAL;
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < 5; k++) {
         int rc = mirsha_ctx_kernel_time(c, k, nullptr, nullptr);
         if (rc) return rc;
         c->timers[k].launches = 0;
@@ -688,13 +917,18 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
         total += len[i];
     }
     const uint64_t span = n_req ? hi - lo : 0;
-    const char* seg_mode = getenv("MIRSHA_PIPELINE_SEGMENTS");
-    const bool pipelined = seg_mode && strcmp(seg_mode, "auto") == 0;  // see plan_segments()
+    // Per-call plans cost host sorting and device allocations, so the host API
+    // uses a plan only when asked (MIRSHA_PIPELINE_MODE=fused|streams); the
+    // device API (mirsha_pipeline_create + *_device) amortises one plan.
+    const char* pmode = getenv("MIRSHA_PIPELINE_MODE");
+    const bool pipelined = pmode && (strcmp(pmode, "fused") == 0 || strcmp(pmode, "streams") == 0 ||
+                                     strcmp(pmode, "auto") == 0);
     if (pipelined && n_batches && n_req && span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES &&
         span <= 2 * total + 4096) {
         mirsha_pipeline p;
         p.device = c->device;
-        int rc = pipeline_build(c, &p, n_req, idx, first, n_batches, len);
+        p.mode = default_pipeline_mode();
+        int rc = plan_build(c, &p, n_req, idx, first, n_batches, len);
         if (rc == MIRSHA_OK) {
             std::vector<uint64_t> roff(off, off + n_req);
             for (auto& x : roff) x -= lo;
@@ -705,8 +939,9 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
             if (span) HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, arena + lo, span, hipMemcpyHostToDevice, c->stream));
             HIP_TRY(c, hipMemcpyAsync(c->d_off.p, roff.data(), sizeof(uint64_t) * n_req, hipMemcpyHostToDevice, c->stream));
             HIP_TRY(c, hipMemcpyAsync(c->d_len.p, len, sizeof(uint32_t) * n_req, hipMemcpyHostToDevice, c->stream));
-            rc = pipeline_run(c, &p, c->d_arena.as<uint8_t>(), span, c->d_off.as<uint64_t>(), c->d_len.as<uint32_t>(),
-                              c->d_out.as<uint8_t>(), c->d_out2.as<uint8_t>());
+            rc = plan_run(c, &p, c->d_arena.as<uint8_t>(), span, c->d_off.as<uint64_t>(), c->d_len.as<uint32_t>(),
+                          c->d_out.as<uint8_t>(), c->d_out2.as<uint8_t>());
+            if (rc == MIRSHA_OK) rc = fused_status(c, &p);
             if (rc == MIRSHA_OK) {
                 HIP_TRY(c, hipMemcpyAsync(batch_out, c->d_out2.p, 32ull * n_batches, hipMemcpyDeviceToHost, c->stream));
                 HIP_TRY(c, hipMemcpyAsync(req_out, c->d_out.p, 32ull * n_req, hipMemcpyDeviceToHost, c->stream));
@@ -732,13 +967,20 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
 
 int mirsha_pipeline_create(mirsha_ctx* c, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
                            const uint32_t* list_first, uint32_t n_lists, mirsha_pipeline** out) {
+    return mirsha_pipeline_create_mode(c, n_req, len, idx, list_first, n_lists, default_pipeline_mode(), out);
+}
+
+int mirsha_pipeline_create_mode(mirsha_ctx* c, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
+                                const uint32_t* list_first, uint32_t n_lists, int mode, mirsha_pipeline** out) {
     if (!c || !out) return MIRSHA_EINVAL;
     *out = nullptr;
+    if (mode < MIRSHA_PIPELINE_SEQUENTIAL || mode > MIRSHA_PIPELINE_AUTO) return fail(c, MIRSHA_EINVAL, "bad mode %d", mode);
     if (int rc = check_lists(c, idx, list_first, n_lists, n_req)) return rc;
     if (int rc = use_device(c)) return rc;
     mirsha_pipeline* p = new mirsha_pipeline();
     p->device = c->device;
-    int rc = pipeline_build(c, p, n_req, idx, list_first, n_lists, len);
+    p->mode = mode;
+    int rc = plan_build(c, p, n_req, idx, list_first, n_lists, len);
     if (rc != MIRSHA_OK) {
         pipeline_free(p);
         delete p;
@@ -753,6 +995,34 @@ void mirsha_pipeline_destroy(mirsha_pipeline* p) {
     (void)hipSetDevice(p->device);
     pipeline_free(p);
     delete p;
+}
+
+int mirsha_pipeline_mode(const mirsha_pipeline* p) { return p ? p->mode : MIRSHA_EINVAL; }
+
+int mirsha_pipeline_trace(mirsha_ctx* c, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words) {
+    if (!c || !p || !words) return MIRSHA_EINVAL;
+    *words = 0;
+    if (p->mode != MIRSHA_PIPELINE_FUSED || !p->trace) return MIRSHA_OK;
+    if (int rc = use_device(c)) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const uint64_t n = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
+    *words = n;
+    if (out && cap) HIP_TRY(c, hipMemcpy(out, p->d_trace.p, 8ull * std::min(n, cap), hipMemcpyDeviceToHost));
+    return MIRSHA_OK;
+}
+
+int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t* n_counters, uint32_t* n_groups) {
+    if (!p || !n_tiles || !n_counters || !n_groups) return MIRSHA_EINVAL;
+    *n_tiles = p->n_tiles;
+    *n_counters = p->n_counters;
+    *n_groups = p->n_groups;
+    return MIRSHA_OK;
+}
+
+int mirsha_pipeline_status(mirsha_ctx* c, mirsha_pipeline* p) {
+    if (!c || !p) return MIRSHA_EINVAL;
+    if (int rc = use_device(c)) return rc;
+    return fused_status(c, p);
 }
 
 int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap) {
@@ -772,7 +1042,7 @@ int mirsha_hash_requests_then_batches_device(mirsha_ctx* c, mirsha_pipeline* p, 
     if (p->n_lists && !d_batch_out) return fail(c, MIRSHA_EINVAL, "NULL batch output");
     if (arena_len > MIRSHA_MAX_DEVICE_ARENA_BYTES) return fail(c, MIRSHA_ERANGE, "device arena too large");
     if (int rc = use_device(c)) return rc;
-    return pipeline_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_batch_out);
+    return plan_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_batch_out);
 }
 
 int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digests, const uint32_t* idx,

@@ -28,6 +28,37 @@ constexpr uint32_t kOpenEnd = 0xFFFFFFFEu;
 hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                         const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
                         uint8_t* out, hipStream_t s);
+// Fused request -> list pass (one persistent launch), see mirsha_kernels.hip.
+constexpr uint32_t kFusedChunkBlocks = 4;  // list blocks (8 digests) per readiness chunk
+constexpr uint32_t kCtlTileTicket = 0, kCtlListTicket = 16, kCtlError = 32, kCtlWords = 48;  // u64 words
+struct FusedArgs {
+    const uint8_t* arena;
+    const uint64_t* off;
+    const uint32_t* len;
+    const uint32_t* order;
+    uint8_t* req_out;
+    const uint32_t* cidx;      // compacted list entries (no null requests)
+    const uint32_t* cfirst;    // n_lists + 1
+    uint8_t* list_out;
+    const uint32_t* tadj_first;  // n_tiles + 1: counters each tile feeds
+    const uint32_t* tadj;
+    const uint32_t* cbase;       // n_groups + 1: first counter of each list group
+    const uint32_t* expected;    // tiles feeding each counter
+    unsigned long long* counters;
+    unsigned long long* ctl;     // kCtlWords: tickets + error flag, one 128-B line each
+    // Optional timeline (s_memrealtime, 100 MHz), NULL = off: per tile [start, end]
+    // at [2t, 2t+1]; per readiness chunk the time its list wave passed the wait
+    // at [2 n_tiles + ctr]; per list group its end at [2 n_tiles + n_counters + g].
+    unsigned long long* trace;
+    uint32_t n_counters;
+    unsigned long long tile_base, list_base;
+    uint32_t arena_len, n_req, n_entries, n_lists;
+    uint32_t epoch, n_tiles, n_groups, list_waves;
+};
+// list_waves = number of list BLOCKS (first in the grid); one block per CU
+// (kPacedLds of reserved LDS), `pace` tile waves per SIMD in tile blocks.
+constexpr uint32_t kPacedLds = 96u * 1024u;
+hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
 hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
                                uint8_t* arena, hipStream_t s);
 

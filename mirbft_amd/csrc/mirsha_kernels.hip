@@ -112,19 +112,32 @@ __device__ __forceinline__ void compress_v(uint32_t st[8], uint32_t w[16]) {
         compress(st, w);
 }
 
-template <bool kLds, bool kAsm>
-__global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
-    const uint8_t* __restrict__ arena, uint32_t arena_len, const uint64_t* __restrict__ off,
-    const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
-    uint8_t* __restrict__ out) {
-    __shared__ uint4 tile[kWavesPerBlock][256];
+// Digest store with the sc1 cache policy: written through to memory (the line
+// leaves this XCD's L2), so a list wave on any XCD can read it with sc1 loads
+// once the storing wave has signalled (MI355X_MICROARCH.md, inter-workgroup
+// visibility: stores and loads all sc1, one atomic add per storing wave).
+constexpr int kSc1 = 1 << 4;  // gfx940+ cache-policy bit: buffer_* ... sc1
 
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t t = blockIdx.x * kWavesPerBlock + wv;
+__device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uint32_t msg, const uint32_t st[8]) {
+    __builtin_amdgcn_raw_buffer_store_b128(
+        (uint32_t __attribute__((ext_vector_type(4)))){__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
+                                                        __builtin_bswap32(st[2]), __builtin_bswap32(st[3])},
+        ors, 32u * msg, 0, kSc1);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        (uint32_t __attribute__((ext_vector_type(4)))){__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
+                                                        __builtin_bswap32(st[6]), __builtin_bswap32(st[7])},
+        ors, 32u * msg + 16u, 0, kSc1);
+}
+
+// One wave hashes the tile of 64 messages at processing positions
+// [64 t, 64 t + 64) (order[] maps a position to a message; NULL = identity).
+// kSc1Out: digests are stored through `ors` with the sc1 policy (fused pass).
+template <bool kLds, bool kAsm, bool kSc1Out>
+__device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint32_t arena_len,
+                                          const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+                                          const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
+                                          __amdgpu_buffer_rsrc_t ors, uint4* my, uint32_t t, uint32_t lane) {
     const uint32_t slot = t * 64u + lane;
-    if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-
     const bool valid = slot < n;
     const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
     const uint32_t L = valid ? len[msg] : 0u;
@@ -153,7 +166,6 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
             oj[j] = (uint32_t)__shfl((int)o, src, 64);
             nbj[j] = (uint32_t)__shfl((int)nb, src, 64);
         }
-        uint4* my = tile[wv];
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
             RawChunk rc[4];
 #pragma unroll
@@ -194,7 +206,27 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
             if (active) compress_v<kAsm>(st, w);
         }
     }
-    if (valid) store_digest(out, msg, st);
+    if (valid) {
+        if constexpr (kSc1Out)
+            store_digest_sc1(ors, msg, st);
+        else
+            store_digest(out, msg, st);
+    }
+}
+
+template <bool kLds, bool kAsm>
+__global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
+    const uint8_t* __restrict__ arena, uint32_t arena_len, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
+    uint8_t* __restrict__ out) {
+    __shared__ uint4 tile[kWavesPerBlock][256];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * kWavesPerBlock + wv;
+    if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
+    hash_tile<kLds, kAsm, false>(arena, arena_len, off, len, order, n, out,
+                                 __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000), tile[wv], t,
+                                 lane);
 }
 
 // Dependent pass: message k = concat(digests[idx[e]] for e in [first[k], first[k+1]))
@@ -403,6 +435,244 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
     }
 }
 
+// ---- fused request -> list pass: ONE launch ---------------------------------
+//
+// The batch / VerifyBatch / checkpoint lists (sequence.go:154-157,
+// batch_tracker.go:147-150) are sequential SHA chains over request digests
+// produced in the same launch.  Request TILES (64 messages) are claimed in
+// order from a ticket; the processing order is the needed-at ordinal of the
+// lists, so every chain's early digests are produced first.  A list GROUP (64
+// lists, one lane each) hashes its lists in chunks of kFusedChunkBlocks
+// blocks; chunk j of group g may start once every tile that feeds it has
+// stored its digests: counter[cbase[g] + j] reaches epoch * expected[...]
+// (each feeding tile adds 1 per run, after its sc1 digest stores completed).
+// Digests are read back with sc1 loads (MI355X_MICROARCH.md, inter-workgroup
+// visibility).  List waves wait only on tile waves, which never wait, so the
+// launch cannot deadlock; a 2 s watchdog per wait raises the error flag
+// instead of hanging if that invariant is ever broken.
+//
+// Tickets are monotone 64-bit counters shared by every run of a plan: each
+// claiming wave makes exactly one failing claim per run, so run r's base is
+// the host-tracked sum of (items + claiming waves) over earlier runs.
+__device__ __forceinline__ uint64_t claim(unsigned long long* ctr, uint32_t lane) {
+    unsigned long long v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, 0, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), 0, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t poll_counter(const unsigned long long* ctr) {
+    return __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load_dwordx2 sc1
+}
+
+// Blocks until *ctr >= target (wave-uniform).  Returns false on watchdog expiry.
+__device__ __noinline__ bool wait_counter(const unsigned long long* ctr, uint64_t target,
+                                          unsigned long long* err) {
+    if (target == 0) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+        const uint64_t v = poll_counter(ctr);
+        if (__shfl((int)(v >= target), 0, 64)) return true;
+        __builtin_amdgcn_s_sleep(8);  // ~512 cycles between polls
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+            __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+}
+
+// Digest `id` via sc1 loads (L1 bypass: another CU wrote it this launch).
+__device__ __forceinline__ void load_digest_sc1(__amdgpu_buffer_rsrc_t rsrc, uint32_t id, bool live, uint4& x0,
+                                                uint4& x1) {
+    const uint32_t o = live ? 32u * id : 0xFFFFFFE0u;
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o, 0, kSc1);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16u, 0, kSc1);
+    x0 = make_uint4(a[0], a[1], a[2], a[3]);
+    x1 = make_uint4(b[0], b[1], b[2], b[3]);
+}
+
+// Chain form of a list group for the paced kernel: a lane's list is consumed
+// a whole readiness chunk (kFusedChunkBlocks blocks = 8 digests) at a time,
+// double-buffered in registers, so one chunk's digest loads (sc1, served from
+// MALL/HBM under full request load: several us) are in flight while the
+// previous chunk is compressed.  Indices are static and loaded a chunk ahead.
+__device__ __forceinline__ void load_chunk_idx(__amdgpu_buffer_rsrc_t irs, uint32_t e0, uint32_t c, uint32_t chunk,
+                                               uint32_t ix[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t o = 8u * chunk + (uint32_t)i;
+        ix[i] = ld_u32(irs, 4u * (e0 + o), o < c);
+    }
+}
+
+__device__ __forceinline__ void load_chunk_digests(__amdgpu_buffer_rsrc_t drs, const uint32_t ix[8], uint32_t c,
+                                                   uint32_t chunk, bool go, uint4 d[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) load_digest_sc1(drs, ix[i], go && 8u * chunk + (uint32_t)i < c, d[2 * i], d[2 * i + 1]);
+}
+
+__device__ __forceinline__ void fused_list_group_deep(const FusedArgs& a, __amdgpu_buffer_rsrc_t drs,
+                                                      __amdgpu_buffer_rsrc_t irs, uint32_t g, uint32_t lane) {
+    static_assert(kFusedChunkBlocks == 4, "chunk = 4 blocks = 8 digests");
+    const uint32_t k = g * 64u + lane;
+    const bool valid = k < a.n_lists;
+    const uint32_t e0 = valid ? a.cfirst[k] : 0u;
+    const uint32_t c = valid ? a.cfirst[k + 1] - e0 : 0u;
+    const uint32_t L = 32u * c;
+    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
+    const uint32_t wave_nb = wave_max(nb);
+    const uint32_t nchunks = (wave_nb + 3u) / 4u;
+    const uint32_t cb = a.cbase[g];
+    auto target = [&](uint32_t chunk) -> uint64_t { return (uint64_t)a.epoch * a.expected[cb + chunk]; };
+    auto stamp = [&](uint32_t at) {
+        if (a.trace && lane == 0) a.trace[at] = __builtin_amdgcn_s_memrealtime();
+    };
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    if (nchunks == 0) {
+        stamp(2u * a.n_tiles + a.n_counters + g);
+        return;
+    }
+    uint32_t ixc[8], ixn[8];
+    load_chunk_idx(irs, e0, c, 0u, ixc);
+    load_chunk_idx(irs, e0, c, 1u, ixn);
+    wait_counter(a.counters + cb, target(0), a.ctl + kCtlError);
+    uint4 dc[16];
+    load_chunk_digests(drs, ixc, c, 0u, true, dc);
+    uint64_t pollv = 1u < nchunks ? poll_counter(a.counters + cb + 1u) : 0u;
+    for (uint32_t chunk = 0; chunk < nchunks; chunk++) {
+        stamp(2u * a.n_tiles + cb + chunk);
+        // Next chunk's digests now if its tiles are done (poll issued one chunk ago).
+        const uint32_t nc = chunk + 1u;
+        bool have_next = false;
+        uint4 dn[16];
+        if (nc < nchunks) {
+            have_next = (bool)__shfl((int)(pollv >= target(nc)), 0, 64);
+            load_chunk_digests(drs, ixn, c, nc, have_next, dn);
+        }
+        uint32_t ixnn[8];
+        load_chunk_idx(irs, e0, c, chunk + 2u, ixnn);
+        if (!have_next && nc + 1u < nchunks) pollv = 0;
+        if (have_next && nc + 1u < nchunks) pollv = poll_counter(a.counters + cb + nc + 1u);
+        else if (nc < nchunks) pollv = poll_counter(a.counters + cb + nc);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t blk = 4u * chunk + (uint32_t)j;
+            if (blk < nb) {
+                uint32_t w[16];
+#pragma unroll
+                for (int half = 0; half < 2; half++) {
+                    const uint32_t di = 2u * blk + (uint32_t)half;
+                    const uint4 x0 = dc[4 * j + 2 * half], x1 = dc[4 * j + 2 * half + 1];
+                    w[8 * half + 0] = __builtin_bswap32(x0.x) | (di == c ? 0x80000000u : 0u);
+                    w[8 * half + 1] = __builtin_bswap32(x0.y); w[8 * half + 2] = __builtin_bswap32(x0.z);
+                    w[8 * half + 3] = __builtin_bswap32(x0.w); w[8 * half + 4] = __builtin_bswap32(x1.x);
+                    w[8 * half + 5] = __builtin_bswap32(x1.y); w[8 * half + 6] = __builtin_bswap32(x1.z);
+                    w[8 * half + 7] = __builtin_bswap32(x1.w);
+                }
+                if (blk + 1u == nb) {
+                    w[14] = L >> 29;
+                    w[15] = L << 3;
+                }
+                compress_asm(st, w);
+            }
+        }
+        stamp(2u * a.n_tiles + a.n_counters + a.n_groups + cb + chunk);
+        if (nc < nchunks) {
+            if (!have_next) {  // exposed: wait for the next chunk's tiles, then load it
+                wait_counter(a.counters + cb + nc, target(nc), a.ctl + kCtlError);
+                load_chunk_digests(drs, ixn, c, nc, true, dn);
+                if (nc + 1u < nchunks) pollv = poll_counter(a.counters + cb + nc + 1u);
+            }
+#pragma unroll
+            for (int i = 0; i < 16; i++) dc[i] = dn[i];
+#pragma unroll
+            for (int i = 0; i < 8; i++) ixn[i] = ixnn[i];
+        }
+    }
+    stamp(2u * a.n_tiles + a.n_counters + g);
+    if (valid) store_digest(a.list_out, k, st);
+}
+
+// Tile loader prefetching kTileDepth blocks ahead (paced kernel: a tile wave is
+// alone on its SIMD, and a load under full request load takes several us).
+constexpr int kTileDepth = 3;
+__device__ __forceinline__ void hash_tile_deep(const uint8_t* __restrict__ arena, uint32_t arena_len,
+                                               const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
+                                               const uint32_t* __restrict__ order, uint32_t n,
+                                               __amdgpu_buffer_rsrc_t ors, uint32_t t, uint32_t lane) {
+    const uint32_t slot = t * 64u + lane;
+    const bool valid = slot < n;
+    const uint32_t msg = valid ? order[slot] : 0u;
+    const uint32_t L = valid ? len[msg] : 0u;
+    const uint32_t o = valid ? (uint32_t)off[msg] : 0u;
+    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
+    const uint32_t wave_nb = wave_max(nb);
+    const uint32_t records = (arena_len + 3u) & ~3u;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)records, 0x00020000);
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    RawChunk rc[kTileDepth][4];
+#pragma unroll
+    for (int d = 0; d < kTileDepth; d++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, (uint32_t)d, (uint32_t)q, (uint32_t)d < nb, rc[d][q]);
+    for (uint32_t blk = 0; blk < wave_nb; blk++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) finish_chunk(rc[0][q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
+#pragma unroll
+        for (int d = 0; d + 1 < kTileDepth; d++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) rc[d][q] = rc[d + 1][q];
+        const uint32_t nbk = blk + (uint32_t)kTileDepth;
+#pragma unroll
+        for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, nbk, (uint32_t)q, nbk < nb, rc[kTileDepth - 1][q]);
+        if (blk < nb) compress_asm(st, w);
+    }
+    if (valid) store_digest_sc1(ors, msg, st);
+}
+
+// Block = 4 x pace waves (pace per SIMD), one block per CU (the launch asks
+// for kPacedLds bytes of LDS it never touches, which keeps any second block
+// off the CU): list blocks [0, list_blocks) run one chain wave per SIMD ALONE
+// on their CU (waves 4.. of a list block exit at once); tile blocks fill the
+// other CUs with `pace` tile waves per SIMD.
+constexpr uint32_t kPacedMaxThreads = 512;
+__global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(FusedArgs a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = threadIdx.x >> 6;
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.req_out, (short)0, (int)(32u * a.n_req), 0x00020000);
+    if (blockIdx.x < a.list_waves) {  // list_waves carries the number of LIST BLOCKS here
+        if (wv >= 4u) return;
+        __builtin_amdgcn_s_setprio(3);
+        const __amdgpu_buffer_rsrc_t irs =
+            __builtin_amdgcn_make_buffer_rsrc((void*)a.cidx, (short)0, (int)(4u * a.n_entries), 0x00020000);
+        while (true) {
+            const uint64_t g = claim(a.ctl + kCtlListTicket, lane) - a.list_base;
+            if (g >= a.n_groups) break;
+            fused_list_group_deep(a, drs, irs, (uint32_t)g, lane);
+        }
+        return;
+    }
+    while (true) {
+        const uint64_t t = claim(a.ctl + kCtlTileTicket, lane) - a.tile_base;
+        if (t >= a.n_tiles) break;
+        if (a.trace && lane == 0) a.trace[2 * t] = __builtin_amdgcn_s_memrealtime();
+        hash_tile_deep(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, drs, (uint32_t)t, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (a.trace && lane == 0) a.trace[2 * t + 1] = __builtin_amdgcn_s_memrealtime();
+        const uint32_t j0 = a.tadj_first[t], j1 = a.tadj_first[t + 1];
+        for (uint32_t j = j0 + lane; j < j1; j += 64u)
+            __hip_atomic_fetch_add(a.counters + a.tadj[j], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -474,6 +744,20 @@ hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32
     const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
     sha256_chain_kernel<<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists, ob, oe,
                                                       state, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    if (pace < 1 || 64u * 4u * pace > kPacedMaxThreads) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute((const void*)sha256_fused_paced_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPacedLds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    sha256_fused_paced_kernel<<<grid, 256u * pace, kPacedLds, s>>>(a);
     return hipGetLastError();
 }
 

@@ -19,6 +19,15 @@ KERNEL_MSGS = 0
 KERNEL_LISTS = 1
 KERNEL_GEN = 2
 KERNEL_CHAIN = 3
+KERNEL_FUSED = 4
+
+# mirsha_pipeline modes (include/mirsha.h)
+PIPELINE_SEQUENTIAL = 0
+PIPELINE_FUSED = 1
+PIPELINE_STREAMS = 2
+PIPELINE_AUTO = 3
+PIPELINE_MODES = {"sequential": PIPELINE_SEQUENTIAL, "fused": PIPELINE_FUSED, "streams": PIPELINE_STREAMS,
+                  "auto": PIPELINE_AUTO}
 VARIANT_LDS = 0
 VARIANT_DIRECT = 1
 VARIANT_LDS_CXX = 2
@@ -192,9 +201,10 @@ class Engine:
         self._check(self._lib.mirsha_digest_lists_device(self.ctx, d_digests, n_digests, d_idx, d_first, n_lists,
                                                          n_entries, d_out))
 
-    def pipeline(self, n_req: int, idx, list_first, length=None) -> "Pipeline":
-        """Plan for request -> batch-digest runs with this list shape (host index lists)."""
-        return Pipeline(self, n_req, idx, list_first, length)
+    def pipeline(self, n_req: int, idx, list_first, length=None, mode: int | str | None = None) -> "Pipeline":
+        """Plan for request -> batch-digest runs with this list shape (host index lists).
+        mode: PIPELINE_AUTO (default) / _FUSED / _SEQUENTIAL / _STREAMS or its name."""
+        return Pipeline(self, n_req, idx, list_first, length, mode)
 
     def hash_requests_then_batches_device(self, plan: "Pipeline", d_arena: int, arena_len: int, d_off: int,
                                           d_len: int, d_req_out: int, d_batch_out: int) -> None:
@@ -206,21 +216,52 @@ class Engine:
 
 
 class Pipeline:
-    """mirsha_pipeline: requests hashed in needed-at chunks, batch chains advanced
-    segment by segment beside them (see include/mirsha.h)."""
+    """mirsha_pipeline: a request -> batch-digest plan reused across runs of one
+    shape (see include/mirsha.h for the modes)."""
 
-    def __init__(self, engine: Engine, n_req: int, idx, list_first, length=None):
+    def __init__(self, engine: Engine, n_req: int, idx, list_first, length=None, mode=None):
         self._lib = engine._lib
         self._engine = engine
         ix = np.ascontiguousarray(idx, dtype=np.uint32)
         fs = np.ascontiguousarray(list_first, dtype=np.uint32)
         ln = None if length is None else np.ascontiguousarray(length, dtype=np.uint32)
         h = ctypes.c_void_p()
-        engine._check(self._lib.mirsha_pipeline_create(engine.ctx, int(n_req), _ptr(ln), _ptr(ix), _ptr(fs),
-                                                       int(fs.size) - 1, ctypes.byref(h)))
+        if mode is None:
+            engine._check(self._lib.mirsha_pipeline_create(engine.ctx, int(n_req), _ptr(ln), _ptr(ix), _ptr(fs),
+                                                           int(fs.size) - 1, ctypes.byref(h)))
+        else:
+            m = PIPELINE_MODES[mode] if isinstance(mode, str) else int(mode)
+            engine._check(self._lib.mirsha_pipeline_create_mode(engine.ctx, int(n_req), _ptr(ln), _ptr(ix),
+                                                                _ptr(fs), int(fs.size) - 1, m, ctypes.byref(h)))
         self.handle = h
+        self.mode = int(self._lib.mirsha_pipeline_mode(h))
         self.n_req = int(n_req)
         self.n_lists = int(fs.size) - 1
+
+    @property
+    def mode_name(self) -> str:
+        return {v: k for k, v in PIPELINE_MODES.items()}[self.mode]
+
+    def status(self) -> None:
+        """Synchronise and raise if a fused run's readiness watchdog expired."""
+        self._engine._check(self._lib.mirsha_pipeline_status(self._engine.ctx, self.handle))
+
+    def shape(self) -> tuple[int, int, int]:
+        """(n_tiles, n_counters, n_groups) of a fused plan."""
+        t, c, g = ctypes.c_uint32(0), ctypes.c_uint32(0), ctypes.c_uint32(0)
+        check(self._lib.mirsha_pipeline_shape(self.handle, ctypes.byref(t), ctypes.byref(c), ctypes.byref(g)))
+        return t.value, c.value, g.value
+
+    def trace(self) -> np.ndarray | None:
+        """Last run's fused timeline (MIRSHA_FUSED_TRACE=1 at plan creation), see include/mirsha.h."""
+        n = ctypes.c_uint64(0)
+        self._engine._check(self._lib.mirsha_pipeline_trace(self._engine.ctx, self.handle, None, 0, ctypes.byref(n)))
+        if n.value == 0:
+            return None
+        out = np.zeros(n.value, dtype=np.uint64)
+        self._engine._check(self._lib.mirsha_pipeline_trace(self._engine.ctx, self.handle, _ptr(out), n.value,
+                                                            ctypes.byref(n)))
+        return out
 
     def segments(self) -> list[int]:
         n = ctypes.c_uint32(0)
@@ -274,6 +315,11 @@ __all__ = [
     "KERNEL_LISTS",
     "KERNEL_GEN",
     "KERNEL_CHAIN",
+    "KERNEL_FUSED",
+    "PIPELINE_SEQUENTIAL",
+    "PIPELINE_FUSED",
+    "PIPELINE_STREAMS",
+    "PIPELINE_AUTO",
     "VARIANT_LDS",
     "VARIANT_DIRECT",
 ]

@@ -41,6 +41,12 @@ def engine():
     broken library must fail the gpu tests loudly."""
     from mirbft_amd import Engine
 
+    # torch's bundled HIP runtime must initialise before the system one that
+    # libmirsha uses, or torch.cuda.is_available() turns False in this process
+    # (measured on the MI355X box); the device-API tests allocate through torch.
+    import torch
+
+    torch.cuda.is_available()
     e = Engine(0)
     yield e
     e.close()

@@ -375,18 +375,41 @@ def test_device_lists_with_nulls_and_empty(engine):
     assert np.array_equal(d_out.cpu().numpy(), oracle_py.batch_digests(dig, idx, first))
 
 
+def _plan_run(engine, plan, arena, off, lens, n_lists, runs=2):
+    """Runs a plan `runs` times on device copies of (arena, off, lens); returns (req, lists)."""
+    torch = _torch()
+    n = lens.size
+    d_arena = torch.from_numpy(np.ascontiguousarray(arena)).cuda()
+    d_off = torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).cuda()
+    d_len = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint32).view(np.int32)).cuda()
+    d_req = torch.empty((max(n, 1), 32), dtype=torch.uint8, device="cuda")
+    d_lst = torch.empty((max(n_lists, 1), 32), dtype=torch.uint8, device="cuda")
+    out = []
+    for _ in range(runs):
+        d_req.zero_()
+        d_lst.zero_()
+        engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), arena.size, d_off.data_ptr(),
+                                                 d_len.data_ptr(), d_req.data_ptr(), d_lst.data_ptr())
+        plan.status()
+        out.append((d_req.cpu().numpy()[:n].copy(), d_lst.cpu().numpy()[:n_lists].copy()))
+    return out
+
+
+@pytest.mark.parametrize("mode", ["auto", "fused", "sequential"])
 @pytest.mark.parametrize("cfg,data_len,n,bs", [(2, 256, 1 << 20, 20), (3, 4096, 1 << 18, 500), (9, 100, 5003, 7)])
-def test_pipeline_device_full_size(engine, cfg, data_len, n, bs):
-    """Pipelined request -> batch digests (needed-at chunks + chain segments on a
-    second stream) at BASELINE sizes, bit-exact vs the oracle, run twice on the
-    same plan (midstate buffers reused)."""
+def test_pipeline_device_full_size(engine, mode, cfg, data_len, n, bs):
+    """Request -> batch digests through a plan at BASELINE sizes (fused: one
+    persistent launch with readiness counters), bit-exact vs the oracle, run
+    twice on the same plan (tickets / counters carried across runs)."""
     torch = _torch()
     stride = 16 + data_len
     seed = synth.SEED_BASE + cfg
     idx, first = sharding.batch_lists(n, bs)
-    plan = engine.pipeline(n, idx, first, np.full(n, stride))
-    segs = plan.segments()
-    assert segs[0] == 0
+    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode=mode)
+    if mode == "auto":  # long VerifyBatch chains -> fused launch; short batches -> two kernels
+        assert plan.mode_name == ("fused" if bs == 500 else "sequential")
+    else:
+        assert plan.mode_name == mode
     d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
     d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
     d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
@@ -401,20 +424,19 @@ def test_pipeline_device_full_size(engine, cfg, data_len, n, bs):
         d_bat.zero_()
         engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
                                                  d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
-        engine.sync()
+        plan.status()
         assert np.array_equal(d_req.cpu().numpy(), want_req)
         assert np.array_equal(d_bat.cpu().numpy(), want_bat)
     plan.close()
 
 
-def test_pipeline_multi_segment_env(engine, monkeypatch):
-    """The experimental multi-segment split (MIRSHA_PIPELINE_SEGMENTS=auto) stays bit-exact."""
-    monkeypatch.setenv("MIRSHA_PIPELINE_SEGMENTS", "auto")
+def test_pipeline_streams_mode(engine):
+    """The two-stream segment split (MIRSHA_PIPELINE_STREAMS) stays bit-exact."""
     torch = _torch()
     n, data_len, bs = 40000, 256, 20
     stride = 16 + data_len
     idx, first = sharding.batch_lists(n, bs)
-    plan = engine.pipeline(n, idx, first, np.full(n, stride))
+    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="streams")
     assert len(plan.segments()) > 1
     d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
     d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
@@ -432,20 +454,66 @@ def test_pipeline_multi_segment_env(engine, monkeypatch):
     plan.close()
 
 
-def test_pipeline_irregular_lists(engine):
-    """Shared requests, unlisted requests, nulls, empty and odd lists through the pipeline."""
-    rng = np.random.default_rng(21)
-    n = 3000
-    lens = rng.integers(0, 600, n).astype(np.uint32)
+def _irregular(seed, n=3000, n_lists=300, max_list=60, max_len=600):
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, max_len, n).astype(np.uint32)
     off = np.zeros(n, dtype=np.uint64)
     np.cumsum(lens[:-1], out=off[1:])
     arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
-    sizes = rng.integers(0, 60, 300)
+    sizes = rng.integers(0, max_list, n_lists)
     sizes[::9] = 0
-    idx = rng.integers(0, n // 2, int(sizes.sum())).astype(np.uint32)  # half the requests unlisted
+    idx = rng.integers(0, max(n // 2, 1), int(sizes.sum())).astype(np.uint32)  # half the requests unlisted
     idx[rng.random(idx.size) < 0.1] = _lib.MIRSHA_NULL_INDEX
     first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    return arena, off, lens, idx, first
+
+
+@pytest.mark.parametrize("env_mode", [None, "fused", "streams", "auto", "sequential"])
+def test_pipeline_irregular_lists(engine, monkeypatch, env_mode):
+    """Shared requests, unlisted requests, nulls, empty and odd lists through the
+    host API (general path, or a per-call plan when MIRSHA_PIPELINE_MODE is set)."""
+    if env_mode:
+        monkeypatch.setenv("MIRSHA_PIPELINE_MODE", env_mode)
+    arena, off, lens, idx, first = _irregular(21)
     req, bat = engine.hash_requests_then_batches(arena, off, lens, idx, first)
     want_req = oracle_py.hash_requests(arena, off, lens)
     assert np.array_equal(req, want_req)
     assert np.array_equal(bat, oracle_py.batch_digests(want_req, idx, first))
+
+
+@pytest.mark.parametrize("seed,n,n_lists,max_list,max_len", [
+    (31, 3000, 300, 60, 600),        # mixed lengths (bucketed order), shared / unlisted / null entries
+    (32, 20000, 70000, 4, 300),      # list groups (1094) > half the grid's waves on small grids: role split
+    (33, 64, 5, 1200, 100),          # few long chains over few tiles, heavy sharing
+    (34, 1, 3, 40, 10),              # one request, repeated in every list
+    (35, 5000, 2, 0, 2000),          # only empty lists (no entries): padding block only
+])
+def test_fused_plan_irregular(engine, seed, n, n_lists, max_list, max_len):
+    """Fused plan (device API) on irregular shapes, three runs on one plan."""
+    arena, off, lens, idx, first = _irregular(seed, n, n_lists, max(max_list, 1), max_len)
+    if max_list == 0:
+        first = np.zeros(n_lists + 1, dtype=np.uint32)
+        idx = np.zeros(0, dtype=np.uint32)
+    plan = engine.pipeline(n, idx, first, lens, mode="fused")
+    want_req = oracle_py.hash_requests(arena, off, lens)
+    want_lst = oracle_py.batch_digests(want_req, idx, first)
+    for req, lst in _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=3):
+        assert np.array_equal(req, want_req)
+        assert np.array_equal(lst, want_lst)
+    plan.close()
+
+
+def test_fused_plans_interleaved(engine):
+    """Two fused plans used alternately: each keeps its own tickets / counters."""
+    a = _irregular(41, 2000, 200, 40, 400)
+    b = _irregular(42, 5000, 90, 300, 200)
+    pa = engine.pipeline(a[2].size, a[3], a[4], a[2], mode="fused")
+    pb = engine.pipeline(b[2].size, b[3], b[4], b[2], mode="fused")
+    for _ in range(2):
+        for (arena, off, lens, idx, first), plan in ((a, pa), (b, pb)):
+            want_req = oracle_py.hash_requests(arena, off, lens)
+            (req, lst), = _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=1)
+            assert np.array_equal(req, want_req)
+            assert np.array_equal(lst, oracle_py.batch_digests(want_req, idx, first))
+    pa.close()
+    pb.close()
