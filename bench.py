@@ -1,15 +1,20 @@
 #!/usr/bin/env python3
 """Benchmark of MirBFT's Actions.Hash hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): synthetic Actions.Hash stream of 2^20
-requests x 256 B data (272-byte messages: LE64(client) || LE64(reqNo) || data,
-state_machine.go:313-317) plus the dependent BatchSize-20 batch digests
-(sequence.go:154-157) computed on device from the device-resident request
-digests.  One step = request digests + batch digests for one such stream.
+Default workload (BASELINE.json configs[1], "config 2"): synthetic Actions.Hash
+stream of 2^20 requests x 256 B data (272-byte messages: LE64(client) ||
+LE64(reqNo) || data, state_machine.go:313-317) plus the dependent BatchSize-20
+batch digests (sequence.go:154-157) computed on device from the
+device-resident request digests.  One step = request digests + batch digests
+for one such stream (one Ready() cycle's Actions.Hash).
+
+Other configs (--config): 3 = 2^18 x 4 KB requests + BatchSize-500
+VerifyBatch digests (batch_tracker.go:147-150); 5 = mixed 64 B - 64 KB
+requests (log-uniform octaves), 12.5M per GPU = 10^8 over 8 GPUs.
 Inputs are generated on device and resident in HBM before the timed region.
 
-Multi-GPU: one process per GPU (torchrun); every rank hashes its own
-request range (weak scaling), no collective in the data path; the barrier and
+Multi-GPU: one process per GPU (torchrun); every rank hashes its own request
+range (weak scaling), no collective in the data path; the barrier and
 max-over-ranks timing use torch.distributed.
 
 Prints ONE JSON line (rank 0).
@@ -42,6 +47,8 @@ CONFIGS = {
     # config id: (data_len, n_requests, batch_size, description)
     2: (256, 1 << 20, 20, "Synthetic Actions.Hash stream: 1M requests x 256 B, BatchSize 20, request + batch digests"),
     3: (4096, 1 << 18, 500, "Large-payload stream: 256K requests x 4 KB, BatchSize 500, VerifyBatch recomputation"),
+    5: (None, 12_500_000, 0, "Mixed-size stream: 64 B - 64 KB requests (log-uniform octaves), "
+                             "12.5M per GPU (10^8 over 8 GPUs), request-range sharded"),
 }
 
 
@@ -56,7 +63,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=100,
                    help="untimed steps; MI355X needs ~20+ ms of sustained load to reach its working clock")
     p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
     p.add_argument("--variant", type=int, default=0, help="0 = LDS-staged loader, 1 = direct per-lane loads")
+    p.add_argument("--windows", action="store_true",
+                   help="config 5: hash in <= 4 GiB windows (one launch each) instead of one 64-bit-addressed launch")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline sample (0 disables)")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-API measurement")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -70,46 +80,11 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(cfg_id, data_len, n_req, bs, seconds):
-    """Oracle (C port of processor.go:133-143 with SHA-NI compression, the
-    instruction class Go's crypto/sha256 uses on amd64) on the host cores."""
+def _oracle():
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_py
+    import oracle_py  # test infrastructure: CPU baseline and self-check only
 
-    stride = 16 + data_len
-    n = min(n_req, 1 << 16)
-    n -= n % bs
-    arena = oracle_py.gen_requests(SEED_BASE + cfg_id, 0, n, data_len)
-    off = np.arange(n, dtype=np.uint64) * stride
-    ln = np.full(n, stride, dtype=np.uint32)
-    idx, first = sharding.batch_lists(n, bs)
-    res = {}
-    for threads in (1, min(16, os.cpu_count() or 1)):
-        done, t0 = 0, time.perf_counter()
-        budget = seconds if threads == 1 else seconds / 3
-        while True:
-            d = oracle_py.hash_requests(arena, off, ln, threads=threads)
-            oracle_py.batch_digests(d, idx, first)
-            done += 1
-            if time.perf_counter() - t0 >= budget:
-                break
-        dt = time.perf_counter() - t0
-        digests = done * (n + first.size - 1)
-        res[threads] = (digests / dt, done, dt)
-    v1, done1, dt1 = res[1]
-    tp = max(k for k in res)
-    return {
-        "value": v1,
-        "unit": "digests/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"{done1} passes x ({n} requests x {stride} B + {first.size - 1} BatchSize-{bs} batch digests), "
-                  f"{dt1:.1f} s, oracle C port of processor.go:133-143 (serial Processor), "
-                  f"SHA-NI compression (stand-in for Go crypto/sha256 amd64 asm)",
-        "pool": {"value": res[tp][0], "threads": tp,
-                 "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361)"},
-        "cpu": _cpu_model(),
-    }
+    return oracle_py
 
 
 def _cpu_model():
@@ -120,6 +95,242 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def _time_cpu(fn, seconds, threads_list):
+    res = {}
+    for threads in threads_list:
+        done, t0 = 0, time.perf_counter()
+        budget = seconds if threads == 1 else seconds / 3
+        while True:
+            fn(threads)
+            done += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        res[threads] = (done, time.perf_counter() - t0)
+    return res
+
+
+class BatchWorkload:
+    """Configs 2 and 3: a dense stream of equal-size requests + batch lists."""
+
+    def __init__(self, a, eng, dev, rank):
+        self.a, self.eng = a, eng
+        self.data_len, n0, self.bs, self.desc = CONFIGS[a.config]
+        self.n = n = a.requests or n0
+        self.stride = stride = 16 + self.data_len
+        self.seed = SEED_BASE + a.config
+        self.first_req = rank * n  # weak scaling: each rank its own request range
+        self.d_arena = torch.empty(n * stride, dtype=torch.uint8, device=dev)
+        self.d_off = torch.arange(n, dtype=torch.int64, device=dev) * stride
+        self.d_len = torch.full((n,), stride, dtype=torch.int32, device=dev)
+        self.d_req = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        self.idx, self.first = sharding.batch_lists(n, self.bs)
+        self.nbat = self.first.size - 1
+        self.d_idx = torch.from_numpy(self.idx.astype(np.int32)).to(dev)
+        self.d_first = torch.from_numpy(self.first.astype(np.int32)).to(dev)
+        self.d_bat = torch.empty((self.nbat, 32), dtype=torch.uint8, device=dev)
+        eng.synth_requests_device(self.seed, self.first_req, n, self.data_len, self.d_arena.data_ptr())
+        self.plan = (eng.pipeline(n, self.idx, self.first, np.full(n, stride), mode=a.pipeline)
+                     if a.pipeline != "none" else None)
+        self.req_blocks = int(blocks(stride)) * n
+        bsz = np.diff(self.first).astype(np.int64) * 32
+        self.bat_blocks = int(blocks(bsz).sum())
+        self.bytes_hashed = n * stride + int(bsz.sum())
+        self.digests = n + self.nbat
+
+    def step(self):
+        e = self.eng
+        if self.plan is not None:
+            e.hash_requests_then_batches_device(self.plan, self.d_arena.data_ptr(), self.d_arena.numel(),
+                                                self.d_off.data_ptr(), self.d_len.data_ptr(), self.d_req.data_ptr(),
+                                                self.d_bat.data_ptr())
+            return
+        e.hash_batch_device(self.d_arena.data_ptr(), self.d_arena.numel(), self.d_off.data_ptr(),
+                            self.d_len.data_ptr(), None, self.n, self.d_req.data_ptr())
+        e.digest_lists_device(self.d_req.data_ptr(), self.n, self.d_idx.data_ptr(), self.d_first.data_ptr(),
+                              self.nbat, int(self.first[-1]), self.d_bat.data_ptr())
+
+    def after(self):
+        if self.plan is not None:
+            self.plan.status()  # raises if a fused run's readiness watchdog ever expired
+
+    def dominant(self):
+        """(kernel name, launches, ms, compressions, algorithmic HBM bytes) of the dominant kernel."""
+        n_f, ms_f = self.eng.kernel_time(KERNEL_FUSED)
+        if n_f:
+            # One launch does the request AND the batch compressions.
+            hbm = self.n * self.stride + self.n * 32 + int(self.first[-1]) * 32 + self.nbat * 32
+            return "sha256_fused_paced_kernel", n_f, ms_f, self.req_blocks + self.bat_blocks, hbm
+        n_m, ms_m = self.eng.kernel_time(KERNEL_MSGS)
+        return "sha256_msgs_kernel", n_m, ms_m, self.req_blocks, self.n * self.stride + self.n * 32
+
+    def batch_ms(self):
+        return self.eng.kernel_time(KERNEL_LISTS)[1] + self.eng.kernel_time(KERNEL_CHAIN)[1]
+
+    def self_check(self):
+        o = _oracle()
+        k = 256
+        arena = o.gen_requests(self.seed, self.first_req, k, self.data_len)
+        want = o.hash_requests(arena, np.arange(k, dtype=np.uint64) * self.stride, np.full(k, self.stride))
+        return bool(np.array_equal(self.d_req[:k].cpu().numpy(), want))
+
+    def pcie(self):
+        n, stride = self.n, self.stride
+        arena_h = self.d_arena.cpu().numpy()
+        off_h = np.arange(n, dtype=np.uint64) * stride
+        len_h = np.full(n, stride, dtype=np.uint32)
+        self.eng.set_stream(None)
+        self.eng.hash_requests_then_batches(arena_h, off_h, len_h, self.idx, self.first)  # warm buffers
+        reps, t1 = 3, time.perf_counter()
+        for _ in range(reps):
+            self.eng.hash_requests_then_batches(arena_h, off_h, len_h, self.idx, self.first)
+        pdt = (time.perf_counter() - t1) / reps
+        return {"digests_per_s": self.digests / pdt, "gb_per_s": self.bytes_hashed / pdt / 1e9,
+                "ms_per_call": pdt * 1e3,
+                "note": "host API (pageable arena -> HBM -> digests -> host), synchronous"}
+
+    def cpu_baseline(self, seconds):
+        """Oracle (C port of processor.go:133-143 with SHA-NI compression, the
+        instruction class Go's crypto/sha256 uses on amd64) on the host cores."""
+        o = _oracle()
+        stride, bs = self.stride, self.bs
+        n = min(self.n, 1 << 16)
+        n -= n % bs
+        arena = o.gen_requests(self.seed, 0, n, self.data_len)
+        off = np.arange(n, dtype=np.uint64) * stride
+        ln = np.full(n, stride, dtype=np.uint32)
+        idx, first = sharding.batch_lists(n, bs)
+
+        def one(threads):
+            d = o.hash_requests(arena, off, ln, threads=threads)
+            o.batch_digests(d, idx, first)
+
+        res = _time_cpu(one, seconds, (1, min(16, os.cpu_count() or 1)))
+        per = n + first.size - 1
+        done1, dt1 = res[1]
+        tp = max(res)
+        return {
+            "value": done1 * per / dt1, "unit": "digests/s", "cores": 1, "kind": "port",
+            "sample": f"{done1} passes x ({n} requests x {stride} B + {first.size - 1} BatchSize-{bs} batch "
+                      f"digests), {dt1:.1f} s, oracle C port of processor.go:133-143 (serial Processor), "
+                      f"SHA-NI compression (stand-in for Go crypto/sha256 amd64 asm)",
+            "pool": {"value": res[tp][0] * per / res[tp][1], "threads": tp,
+                     "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361)"},
+            "cpu": _cpu_model(),
+        }
+
+    def config_fields(self):
+        return {"requests_per_gpu": self.n, "request_bytes": self.stride, "batch_size": self.bs,
+                "batch_digests_per_gpu": self.nbat,
+                "compressions_per_step_per_gpu": self.req_blocks + self.bat_blocks,
+                "pipeline": self.a.pipeline if self.plan is None else f"{self.a.pipeline} -> {self.plan.mode_name}",
+                }
+
+    def extra(self):
+        mode = self.plan.mode_name if self.plan is not None else "none"
+        return {"batch_kernel_avg_ms": self.batch_ms() / self.a.steps,
+                "batch_pass": {"none": "sequential batch kernel (plain device API)",
+                               "fused": "fused into the request launch (readiness counters, no second kernel)",
+                               "sequential": "plan: request kernel then batch kernel",
+                               "streams": "chain segments on a second stream"}[mode]}
+
+
+class MixedWorkload:
+    """Config 5: 64 B - 64 KB requests packed densely in HBM (~123 GB per GPU at
+    12.5M requests), hashed in ONE launch (64-bit per-lane addressing) in a
+    global longest-first length-bucketed order, so the long chains start first
+    and the launch's tail is short messages; --windows: <= 4 GiB origin-order
+    windows, one launch each (A/B)."""
+
+    def __init__(self, a, eng, dev, rank):
+        self.a, self.eng = a, eng
+        _, n0, _, self.desc = CONFIGS[5]
+        self.n = n = a.requests or n0
+        self.seed = SEED_BASE + 5
+        self.first_req = rank * n
+        d_len = torch.empty(n, dtype=torch.int32, device=dev)
+        eng.synth_mixed_lengths_device(self.seed, self.first_req, n, d_len.data_ptr())
+        eng.sync()
+        self.ln = d_len.cpu().numpy().view(np.uint32)
+        self.off = np.zeros(n, dtype=np.uint64)
+        np.cumsum(self.ln[:-1], out=self.off[1:])
+        self.total = int(self.off[-1]) + int(self.ln[-1])
+        if a.windows:
+            self.wins = sharding.arena_windows(self.off, self.ln)
+        else:
+            self.wins = [(0, n, 0)]
+        offrel = self.off.copy()
+        for i0, i1, base in self.wins:
+            offrel[i0:i1] -= np.uint64(base)
+        order = sharding.window_orders(self.ln, self.wins)
+        self.d_len = d_len
+        self.d_off = torch.from_numpy(self.off.view(np.int64)).to(dev)
+        self.d_offrel = torch.from_numpy(offrel.view(np.int64)).to(dev) if a.windows else self.d_off
+        self.d_order = torch.from_numpy(order.view(np.int32)).to(dev)
+        self.d_arena = torch.empty(self.total + 256, dtype=torch.uint8, device=dev)
+        self.d_req = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+        eng.synth_mixed_device(self.seed, self.first_req, n, self.d_off.data_ptr(), self.d_arena.data_ptr())
+        eng.sync()
+        self.req_blocks = int(blocks(self.ln).sum())
+        self.bytes_hashed = self.total
+        self.digests = n
+        self.plan = None
+
+    def step(self):
+        e = self.eng
+        ap, op, lp = self.d_arena.data_ptr(), self.d_offrel.data_ptr(), self.d_len.data_ptr()
+        rp, qp = self.d_order.data_ptr(), self.d_req.data_ptr()
+        for i0, i1, base in self.wins:
+            span = int(self.off[i1 - 1]) + int(self.ln[i1 - 1]) - base
+            e.hash_batch_device(ap + base, span, op + 8 * i0, lp + 4 * i0, rp + 4 * i0, i1 - i0, qp + 32 * i0)
+
+    def after(self):
+        pass
+
+    def dominant(self):
+        n_m, ms_m = self.eng.kernel_time(KERNEL_MSGS)
+        return "sha256_msgs_kernel", n_m, ms_m, self.req_blocks, self.total + 32 * self.n
+
+    def self_check(self):
+        o = _oracle()
+        rng = np.random.default_rng(5)
+        ids = np.sort(rng.choice(self.n, size=min(256, self.n), replace=False))
+        arena, off, ln = o.gen_mixed(self.seed, ids + self.first_req)
+        if not np.array_equal(ln, self.ln[ids]):
+            return False
+        want = o.hash_requests(arena, off, ln)
+        got = self.d_req[torch.from_numpy(ids.astype(np.int64)).to(self.d_req.device)].cpu().numpy()
+        return bool(np.array_equal(got, want))
+
+    def pcie(self):
+        return None  # ~123 GB per GPU: the host API path is not measured for this config
+
+    def cpu_baseline(self, seconds):
+        o = _oracle()
+        k = min(self.n, 30000)  # ~300 MB sample of the same stream
+        arena, off, ln = o.gen_mixed(self.seed, np.arange(k, dtype=np.uint64))
+        res = _time_cpu(lambda t: o.hash_requests(arena, off, ln, threads=t), seconds,
+                        (1, min(16, os.cpu_count() or 1)))
+        done1, dt1 = res[1]
+        tp = max(res)
+        return {
+            "value": done1 * k / dt1, "unit": "digests/s", "cores": 1, "kind": "port",
+            "gb_per_s": done1 * int(ln.sum()) / dt1 / 1e9,
+            "sample": f"{done1} passes x {k} mixed requests ({int(ln.sum()) / 1e6:.0f} MB), {dt1:.1f} s, oracle C "
+                      f"port of processor.go:133-143, SHA-NI compression",
+            "pool": {"value": res[tp][0] * k / res[tp][1], "threads": tp},
+            "cpu": _cpu_model(),
+        }
+
+    def config_fields(self):
+        return {"requests_per_gpu": self.n, "arena_gb_per_gpu": self.total / 1e9,
+                "mean_request_bytes": self.total / self.n, "launches_per_step": len(self.wins),
+                "addressing": "4 GiB windows" if self.a.windows else "one launch, 64-bit per-lane addresses",
+                "compressions_per_step_per_gpu": self.req_blocks}
+
+    def extra(self):
+        return {}
 
 
 def main():
@@ -137,41 +348,16 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    data_len, n, bs, desc = CONFIGS[a.config]
-    stride = 16 + data_len
-    first_req = rank * n  # weak scaling: each rank its own request range
-
     eng = Engine(local)
     eng.set_variant(a.variant)
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
 
-    d_arena = torch.empty(n * stride, dtype=torch.uint8, device=dev)
-    d_off = torch.arange(n, dtype=torch.int64, device=dev) * stride
-    d_len = torch.full((n,), stride, dtype=torch.int32, device=dev)
-    d_req = torch.empty((n, 32), dtype=torch.uint8, device=dev)
-    idx, first = sharding.batch_lists(n, bs)
-    nbat = first.size - 1
-    d_idx = torch.from_numpy(idx.astype(np.int32)).to(dev)
-    d_first = torch.from_numpy(first.astype(np.int32)).to(dev)
-    d_bat = torch.empty((nbat, 32), dtype=torch.uint8, device=dev)
-    eng.synth_requests_device(SEED_BASE + a.config, first_req, n, data_len, d_arena.data_ptr())
+    wl = (MixedWorkload if a.config == 5 else BatchWorkload)(a, eng, dev, rank)
     torch.cuda.synchronize(dev)
 
-    plan = eng.pipeline(n, idx, first, np.full(n, stride), mode=a.pipeline) if a.pipeline != "none" else None
-
-    def step():
-        if plan is not None:
-            eng.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
-                                                  d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
-            return
-        eng.hash_batch_device(d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr(), None, n,
-                              d_req.data_ptr())
-        eng.digest_lists_device(d_req.data_ptr(), n, d_idx.data_ptr(), d_first.data_ptr(), nbat, int(first[-1]),
-                                d_bat.data_ptr())
-
     for _ in range(a.warmup):
-        step()
+        wl.step()
     torch.cuda.synchronize(dev)
 
     def timed(with_events):
@@ -182,7 +368,7 @@ def main():
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            step()
+            wl.step()
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
@@ -191,16 +377,10 @@ def main():
         return el
 
     dt = timed(bool(a.events_in_timed_loop))
-    dt_bare = None
     if not a.events_in_timed_loop:
-        dt_bare = dt
         timed(True)
-    n_msgs, ms_msgs = eng.kernel_time(KERNEL_MSGS)
-    n_lists, ms_lists = eng.kernel_time(KERNEL_LISTS)
-    n_chain, ms_chain = eng.kernel_time(KERNEL_CHAIN)
-    n_fused, ms_fused = eng.kernel_time(KERNEL_FUSED)
-    if plan is not None:
-        plan.status()  # raises if a fused run's readiness watchdog ever expired
+    wl.after()
+    kname, n_k, ms_k, work_blocks, hbm_bytes = wl.dominant()
 
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -208,38 +388,13 @@ def main():
         dt = float(t.item())
 
     # quick self-check of the last step against the CPU oracle on a sample
-    check_ok = None
-    if rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_py
+    check_ok = wl.self_check() if rank == 0 else None
 
-        k = 256
-        arena = oracle_py.gen_requests(SEED_BASE + a.config, first_req, k, data_len)
-        want = oracle_py.hash_requests(arena, np.arange(k, dtype=np.uint64) * stride, np.full(k, stride))
-        check_ok = bool(np.array_equal(d_req[:k].cpu().numpy(), want))
-
-    # algorithmic totals per step (per rank)
-    req_blocks = int(blocks(stride)) * n
-    bsz = np.diff(first).astype(np.int64) * 32
-    bat_blocks = int(blocks(bsz).sum())
-    bytes_hashed = n * stride + int(bsz.sum())
-    digests_per_step = n + nbat
-    value = digests_per_step * world * a.steps / dt
-    gbps = bytes_hashed * world * a.steps / dt / 1e9
-
-    fused = n_fused > 0
-    if fused:
-        # One persistent launch does the request AND the batch compressions.
-        kname, n_k, ms_k, work_blocks = "sha256_fused_paced_kernel", n_fused, ms_fused, req_blocks + bat_blocks
-        hbm_bytes = n * stride + n * 32 + int(first[-1]) * 32 + nbat * 32
-    else:
-        kname, n_k, ms_k, work_blocks = "sha256_msgs_kernel", n_msgs, ms_msgs, req_blocks
-        hbm_bytes = n * stride + n * 32
-    avg_msgs_ms = ms_k / max(n_k, 1)
-    msgs_ms_per_step = ms_k / a.steps  # all launches of the dominant kernel in one step
-    avg_lists_ms = (ms_lists + ms_chain) / a.steps  # separate dependent pass device time per step
-    achieved_tops = work_blocks * OPS_PER_COMPRESSION / (msgs_ms_per_step * 1e-3) / 1e12
-    hbm_gbs = hbm_bytes / (msgs_ms_per_step * 1e-3) / 1e9
+    value = wl.digests * world * a.steps / dt
+    gbps = wl.bytes_hashed * world * a.steps / dt / 1e9
+    ms_per_step_k = ms_k / a.steps  # all launches of the dominant kernel in one step
+    achieved_tops = work_blocks * OPS_PER_COMPRESSION / (ms_per_step_k * 1e-3) / 1e12
+    hbm_gbs = hbm_bytes / (ms_per_step_k * 1e-3) / 1e9
 
     traffic = None
     if os.path.exists(a.traffic_file):
@@ -249,24 +404,8 @@ def main():
         except (OSError, ValueError):
             traffic = None
 
-    pcie = None
-    if rank == 0 and world == 1 and not a.no_pcie:
-        arena_h = d_arena.cpu().numpy()
-        off_h = np.arange(n, dtype=np.uint64) * stride
-        len_h = np.full(n, stride, dtype=np.uint32)
-        eng.set_stream(None)
-        eng.hash_requests_then_batches(arena_h, off_h, len_h, idx, first)  # warm buffers
-        reps, t1 = 3, time.perf_counter()
-        for _ in range(reps):
-            eng.hash_requests_then_batches(arena_h, off_h, len_h, idx, first)
-        pdt = (time.perf_counter() - t1) / reps
-        pcie = {"digests_per_s": digests_per_step / pdt, "gb_per_s": bytes_hashed / pdt / 1e9,
-                "ms_per_call": pdt * 1e3,
-                "note": "host API (pageable arena -> HBM -> digests -> host), synchronous"}
-
-    cpu = None
-    if rank == 0 and world == 1 and a.cpu_seconds > 0:
-        cpu = cpu_baseline(a.config, data_len, n, bs, a.cpu_seconds)
+    pcie = wl.pcie() if rank == 0 and world == 1 and not a.no_pcie else None
+    cpu = wl.cpu_baseline(a.cpu_seconds) if rank == 0 and world == 1 and a.cpu_seconds > 0 else None
 
     if rank == 0:
         line = {
@@ -283,15 +422,10 @@ def main():
             "dtype": "u32",
             "data": "synthetic (splitmix64 request stream generated on device, SURVEY.md §8d)",
             "config": {
-                "workload": f"config{a.config}: {desc}",
-                "requests_per_gpu": n,
-                "request_bytes": stride,
-                "batch_size": bs,
-                "batch_digests_per_gpu": nbat,
-                "compressions_per_step_per_gpu": req_blocks + bat_blocks,
+                "workload": f"config{a.config}: {wl.desc}",
+                **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
                 "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx"][a.variant],
-                "pipeline": a.pipeline if plan is None else f"{a.pipeline} -> {plan.mode_name}",
             },
             "gb_per_s_hashed": gbps,
             "roofline": {
@@ -302,21 +436,16 @@ def main():
                 "frac": achieved_tops / VALU_PEAK_TOPS,
                 "traffic": traffic,
                 "kernel": kname,
-                "avg_launch_ms": avg_msgs_ms,
+                "avg_launch_ms": ms_k / max(n_k, 1),
                 "launches_per_step": n_k / a.steps,
-                "kernel_ms_per_step": msgs_ms_per_step,
+                "kernel_ms_per_step": ms_per_step_k,
                 "work": f"{work_blocks} compressions x {OPS_PER_COMPRESSION} int32 ops per step "
                         f"(over {n_k // a.steps} launch(es))",
                 "hbm_algorithmic_gb_per_s": hbm_gbs,
                 "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
                 "note": "SHA-256 is int32 VALU work (no MFMA shape); hbm/mfma bounds do not apply",
             },
-            "batch_kernel_avg_ms": avg_lists_ms,
-            "batch_pass": {"none": "sequential batch kernel (plain device API)",
-                           "fused": "fused into the request launch (readiness counters, no second kernel)",
-                           "sequential": "plan: request kernel then batch kernel",
-                           "streams": "chain segments %s on a second stream" % (plan.segments() if plan else None),
-                           }[plan.mode_name if plan is not None else "none"],
+            **wl.extra(),
             "events_in_timed_loop": bool(a.events_in_timed_loop),
             "self_check": check_ok,
             "pcie_inclusive": pcie,

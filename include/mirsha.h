@@ -128,9 +128,13 @@ int mirsha_digest_lists(mirsha_ctx* ctx, const uint8_t* digests, uint32_t n_dige
 
 /* -------------------------------------------------------------- device API */
 /* All pointers are device pointers; asynchronous on the context stream.
- * arena_len <= MIRSHA_MAX_DEVICE_ARENA_BYTES; reads past arena_len return 0.
- * order (may be NULL) lists message indices in processing order, e.g. from
- * mirsha_bucket_order; NULL = identity. */
+ * Reads past arena_len return 0.  Any arena size: up to
+ * MIRSHA_MAX_DEVICE_ARENA_BYTES one 32-bit buffer descriptor addresses it,
+ * beyond that (BASELINE config 5: ~123 GB per GPU in one launch) the loader
+ * switches to 64-bit per-lane addresses.  order (may be NULL) lists message
+ * indices in processing order, e.g. from mirsha_bucket_order (longest first:
+ * with mixed sizes this keeps the long chains off the launch's tail); NULL =
+ * identity. */
 int mirsha_hash_batch_device(mirsha_ctx* ctx, const uint8_t* d_arena, uint64_t arena_len,
                              const uint64_t* d_off, const uint32_t* d_len,
                              const uint32_t* d_order, uint32_t n, uint8_t* d_digests_out);
@@ -216,6 +220,15 @@ int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena,
  * splitmix64(splitmix64(seed ^ i) + j).  count messages packed densely. */
 int mirsha_synth_requests_device(mirsha_ctx* ctx, uint64_t seed, uint64_t first, uint64_t count,
                                  uint32_t data_len, uint8_t* d_arena);
+/* BASELINE config 5 stream (mixed 64 B - 64 KB): d_len[r] = message length
+ * (16 + data_len) of request first + r, data_len log-uniform over the octaves
+ * of [64, 65536) in integer arithmetic (identical to the oracle's
+ * oracle_mixed_data_len); then the message bytes (same layout and data as
+ * above) at d_arena + d_off[r], any byte alignment. */
+int mirsha_synth_mixed_lengths_device(mirsha_ctx* ctx, uint64_t seed, uint64_t first, uint64_t count,
+                                      uint32_t* d_len);
+int mirsha_synth_mixed_device(mirsha_ctx* ctx, uint64_t seed, uint64_t first, uint64_t count,
+                              const uint64_t* d_off, uint8_t* d_arena);
 
 #ifdef __cplusplus
 }

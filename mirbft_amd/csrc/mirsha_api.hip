@@ -218,7 +218,7 @@ int hash_resident(mirsha_ctx* c, const uint8_t* d_arena, uint64_t arena_len, con
         d_order = c->d_order.as<uint32_t>();
     }
     int rc = timed_launch(c, 0, [&] {
-        return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, c->d_off.as<uint64_t>(),
+        return mirsha::launch_msgs(d_arena, arena_len, c->d_off.as<uint64_t>(),
                                    c->d_len.as<uint32_t>(), d_order, n, d_out, c->variant, c->stream);
     });
     if (rc) return rc;
@@ -454,7 +454,7 @@ int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint
         const uint32_t n = p->chunk_begin[S + 1];
         if (n) {
             if (int rc = timed_launch(c, 0, [&] {
-                    return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, d_off, d_len, order, n, d_req_out,
+                    return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, order, n, d_req_out,
                                                c->variant, c->stream);
                 }))
                 return rc;
@@ -474,7 +474,7 @@ int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint
         const uint32_t b = p->chunk_begin[s], n = p->chunk_begin[s + 1] - b;
         if (n) {
             if (int rc = timed_launch(c, 0, [&] {
-                    return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, d_off, d_len, order + b, n, d_req_out,
+                    return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, order + b, n, d_req_out,
                                                c->variant, c->stream);
                 }))
                 return rc;
@@ -1069,12 +1069,9 @@ int mirsha_hash_batch_device(mirsha_ctx* c, const uint8_t* d_arena, uint64_t are
     if (!c) return MIRSHA_EINVAL;
     if (n == 0) return MIRSHA_OK;
     if (!d_off || !d_len || !d_out || (!d_arena && arena_len)) return fail(c, MIRSHA_EINVAL, "NULL argument");
-    if (arena_len > MIRSHA_MAX_DEVICE_ARENA_BYTES)
-        return fail(c, MIRSHA_ERANGE, "device arena %llu bytes > %u", (unsigned long long)arena_len,
-                    MIRSHA_MAX_DEVICE_ARENA_BYTES);
     if (int rc = use_device(c)) return rc;
     return timed_launch(c, 0, [&] {
-        return mirsha::launch_msgs(d_arena, (uint32_t)arena_len, d_off, d_len, d_order, n, d_out, c->variant,
+        return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, d_order, n, d_out, c->variant,
                                    c->stream);
     });
 }
@@ -1097,6 +1094,22 @@ int mirsha_digest_lists_device(mirsha_ctx* c, const uint8_t* d_digests, uint32_t
 int mirsha_bucket_order(const uint32_t* len, uint32_t n, uint32_t* order_out) {
     if (n && (!len || !order_out)) return MIRSHA_EINVAL;
     return bucket_order(len, n, order_out) ? 1 : 0;
+}
+
+int mirsha_synth_mixed_lengths_device(mirsha_ctx* c, uint64_t seed, uint64_t first, uint64_t count,
+                                      uint32_t* d_len) {
+    if (!c) return MIRSHA_EINVAL;
+    if (count && !d_len) return fail(c, MIRSHA_EINVAL, "NULL length buffer");
+    if (int rc = use_device(c)) return rc;
+    return timed_launch(c, 2, [&] { return mirsha::launch_mixed_lengths(seed, first, count, d_len, c->stream); });
+}
+
+int mirsha_synth_mixed_device(mirsha_ctx* c, uint64_t seed, uint64_t first, uint64_t count, const uint64_t* d_off,
+                              uint8_t* d_arena) {
+    if (!c) return MIRSHA_EINVAL;
+    if (count && (!d_off || !d_arena)) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (int rc = use_device(c)) return rc;
+    return timed_launch(c, 2, [&] { return mirsha::launch_gen_mixed(seed, first, count, d_off, d_arena, c->stream); });
 }
 
 int mirsha_synth_requests_device(mirsha_ctx* c, uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,

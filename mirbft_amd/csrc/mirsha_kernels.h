@@ -13,7 +13,10 @@ constexpr uint32_t kNullIndex = 0xFFFFFFFFu;
 // rounds (generated asm / compiler-scheduled C++).  Default: kVariantLds.
 enum : int { kVariantLds = 0, kVariantDirect = 1, kVariantLdsCxx = 2, kVariantDirectCxx = 3 };
 
-hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t* off,
+// Arenas up to kMaxBufferArena bytes use one 32-bit buffer descriptor; larger
+// ones (any size) the 64-bit per-lane addressed loader.
+constexpr uint64_t kMaxBufferArena = 0xFFFFFF00ull;
+hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
                        const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
                        int variant, hipStream_t s);
 // scratch: device buffer with at least first[n_lists] entries (null compaction).
@@ -61,5 +64,8 @@ constexpr uint32_t kPacedLds = 96u * 1024u;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
 hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
                                uint8_t* arena, hipStream_t s);
+hipError_t launch_mixed_lengths(uint64_t seed, uint64_t first, uint64_t count, uint32_t* len, hipStream_t s);
+hipError_t launch_gen_mixed(uint64_t seed, uint64_t first, uint64_t count, const uint64_t* off, uint8_t* arena,
+                            hipStream_t s);
 
 }  // namespace mirsha

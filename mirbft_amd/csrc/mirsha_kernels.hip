@@ -16,6 +16,8 @@
 // on the tail chunks, and writes them into the wave's private 4 KiB LDS tile,
 // XOR-swizzled so both the ds_write_b128 (8-lane groups, 128 contiguous bytes)
 // and the per-lane ds_read_b128 (16-lane groups) are bank-conflict free.
+#include <algorithm>
+
 #include "mirsha_kernels.h"
 #include "sha256_device.h"
 
@@ -64,6 +66,32 @@ __device__ __forceinline__ void issue_chunk(__amdgpu_buffer_rsrc_t rsrc, uint32_
             : "=&v"(c.v[0]), "=&v"(c.v[1]), "=&v"(c.v[2]), "=&v"(c.v[3]), "=&v"(c.v[4])
             : "v"(a), "s"(rsrc)
             : "memory");
+    }
+}
+
+// The same raw chunk through 64-bit per-lane global addresses, for arenas
+// beyond one buffer descriptor's 32-bit reach (> 4 GiB per launch, BASELINE
+// config 5).  Same semantics: inactive chunks and dwords past `records`
+// (arena_len rounded up to 4) read as zero without a memory access.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+__device__ __forceinline__ void issue_chunk_wide(const uint8_t* __restrict__ arena, uint64_t records, uint64_t o,
+                                                 uint32_t blk, uint32_t q, bool active, RawChunk& c) {
+    const uint64_t addr = o + 64ull * blk + 16u * q;
+    const uint64_t a = addr & ~3ull;
+    c.sel = be_sel((uint32_t)addr & 3u);
+#pragma unroll
+    for (int k = 0; k < 5; k++) c.v[k] = 0u;
+    if (active) {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(arena + a);
+        if (a + 20u <= records) {
+            const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(p);
+            c.v[0] = v[0]; c.v[1] = v[1]; c.v[2] = v[2]; c.v[3] = v[3];
+            c.v[4] = p[4];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                if (a + 4u * k + 4u <= records) c.v[k] = p[k];
+        }
     }
 }
 
@@ -132,8 +160,8 @@ __device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uin
 // One wave hashes the tile of 64 messages at processing positions
 // [64 t, 64 t + 64) (order[] maps a position to a message; NULL = identity).
 // kSc1Out: digests are stored through `ors` with the sc1 policy (fused pass).
-template <bool kLds, bool kAsm, bool kSc1Out>
-__device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint32_t arena_len,
+template <bool kLds, bool kAsm, bool kSc1Out, bool kWide = false>
+__device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
                                           __amdgpu_buffer_rsrc_t ors, uint4* my, uint32_t t, uint32_t lane) {
@@ -141,15 +169,21 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     const bool valid = slot < n;
     const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
     const uint32_t L = valid ? len[msg] : 0u;
-    const uint32_t o = valid ? (uint32_t)off[msg] : 0u;
+    const uint64_t o = valid ? off[msg] : 0u;
     const uint32_t nb = valid ? blocks_for_len(L) : 0u;
     const uint32_t wave_nb = wave_max(nb);
 
     // Bytes past arena_len inside the last dword are never part of a message
     // (they are masked by the padding logic), so the range rounds up to 4.
-    const uint32_t records = (arena_len + 3u) & ~3u;
+    const uint64_t records = (arena_len + 3u) & ~3ull;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)records, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)(uint32_t)records, 0x00020000);
+    auto issue = [&](uint64_t mo, uint32_t blk, uint32_t q, bool active, RawChunk& rc) {
+        if constexpr (kWide)
+            issue_chunk_wide(arena, records, mo, blk, q, active, rc);
+        else
+            issue_chunk(rsrc, (uint32_t)records, (uint32_t)mo, blk, q, active, rc);
+    };
 
     uint32_t st[8];
 #pragma unroll
@@ -158,18 +192,20 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     if constexpr (kLds) {
         // Loader roles: this lane fetches quarter q of messages m_j = 16j + lane/4.
         const uint32_t q = lane & 3u;
-        uint32_t Lj[4], oj[4], nbj[4];
+        uint32_t Lj[4], nbj[4];
+        uint64_t oj[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int src = 16 * j + (int)(lane >> 2);
             Lj[j] = (uint32_t)__shfl((int)L, src, 64);
-            oj[j] = (uint32_t)__shfl((int)o, src, 64);
+            oj[j] = (uint64_t)(uint32_t)__shfl((int)(uint32_t)o, src, 64);
+            if constexpr (kWide) oj[j] |= (uint64_t)(uint32_t)__shfl((int)(uint32_t)(o >> 32), src, 64) << 32;
             nbj[j] = (uint32_t)__shfl((int)nb, src, 64);
         }
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
             RawChunk rc[4];
 #pragma unroll
-            for (int j = 0; j < 4; j++) issue_chunk(rsrc, records, oj[j], blk, q, blk < nbj[j], rc[j]);
+            for (int j = 0; j < 4; j++) issue(oj[j], blk, q, blk < nbj[j], rc[j]);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 uint32_t wq[4];
@@ -198,7 +234,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             const bool active = blk < nb;
             RawChunk rc[4];
 #pragma unroll
-            for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, blk, (uint32_t)q, active, rc[q]);
+            for (int q = 0; q < 4; q++) issue(o, blk, (uint32_t)q, active, rc[q]);
             uint32_t w[16];
 #pragma unroll
             for (int q = 0; q < 4; q++)
@@ -214,9 +250,9 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     }
 }
 
-template <bool kLds, bool kAsm>
+template <bool kLds, bool kAsm, bool kWide = false>
 __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
-    const uint8_t* __restrict__ arena, uint32_t arena_len, const uint64_t* __restrict__ off,
+    const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
     uint8_t* __restrict__ out) {
     __shared__ uint4 tile[kWavesPerBlock][256];
@@ -224,7 +260,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * kWavesPerBlock + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<kLds, kAsm, false>(arena, arena_len, off, len, order, n, out,
+    hash_tile<kLds, kAsm, false, kWide>(arena, arena_len, off, len, order, n, out,
                                  __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000), tile[wv], t,
                                  lane);
 }
@@ -704,13 +740,53 @@ __global__ void gen_requests_kernel(uint64_t seed, uint64_t first, uint64_t coun
     for (uint32_t b = 0; b < nbytes; b++) m[base + b] = (uint8_t)(v >> (8 * b));
 }
 
+// BASELINE config 5 (mixed 64 B - 64 KB requests): data length
+// of request i, integer-only so host (oracle_mixed_data_len), numpy and
+// device agree bit for bit: log-uniform over the octaves of [64, 65536),
+// uniform inside an octave.
+constexpr uint64_t kLenTag = 0x4C454E4754480000ull;
+__device__ __forceinline__ uint32_t mixed_data_len(uint64_t seed, uint64_t i) {
+    const uint64_t x = splitmix64(seed ^ i ^ kLenTag) >> 40;
+    const uint64_t t = 10u * x;
+    const uint64_t e = t >> 24, m = t & 0xFFFFFFu;
+    return (uint32_t)((64ull << e) + (((64ull << e) * m) >> 24));
+}
+
+__global__ void mixed_lengths_kernel(uint64_t seed, uint64_t first, uint64_t count, uint32_t* __restrict__ len) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < count) len[r] = 16u + mixed_data_len(seed, first + r);
+}
+
+// One wave per message (grid-stride), lanes over its 8-byte words; byte
+// stores because messages are packed at any byte alignment.
+__global__ void gen_mixed_kernel(uint64_t seed, uint64_t first, uint64_t count, const uint64_t* __restrict__ off,
+                                 uint8_t* __restrict__ arena) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t r = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < count; r += waves) {
+        const uint64_t i = first + r;
+        const uint32_t L = 16u + mixed_data_len(seed, i);
+        const uint64_t key = splitmix64(seed ^ i);
+        uint8_t* m = arena + off[r];
+        for (uint32_t w = lane; 8u * w < L; w += 64u) {
+            const uint64_t v = w == 0 ? i % 16u : (w == 1 ? i / 16u : splitmix64(key + (w - 2u)));
+            const uint32_t nbytes = L - 8u * w < 8u ? L - 8u * w : 8u;
+            for (uint32_t b = 0; b < nbytes; b++) m[8u * w + b] = (uint8_t)(v >> (8 * b));
+        }
+    }
+}
+
 // ---- host-side launchers --------------------------------------------------
-hipError_t launch_msgs(const uint8_t* arena, uint32_t arena_len, const uint64_t* off,
+hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
                        const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
                        int variant, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t tiles = (n + 63u) / 64u;
     const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
+    if (arena_len > kMaxBufferArena) {  // 64-bit per-lane addressing (LDS loader, asm rounds)
+        sha256_msgs_kernel<true, true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        return hipGetLastError();
+    }
     switch (variant) {
         case kVariantLds:
             sha256_msgs_kernel<true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
@@ -758,6 +834,20 @@ hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, 
         attr = true;
     }
     sha256_fused_paced_kernel<<<grid, 256u * pace, kPacedLds, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_mixed_lengths(uint64_t seed, uint64_t first, uint64_t count, uint32_t* len, hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    mixed_lengths_kernel<<<(unsigned)((count + 255u) / 256u), 256, 0, s>>>(seed, first, count, len);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_mixed(uint64_t seed, uint64_t first, uint64_t count, const uint64_t* off, uint8_t* arena,
+                            hipStream_t s) {
+    if (count == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((count + 3u) / 4u, 65536u);
+    gen_mixed_kernel<<<(unsigned)blocks, 256, 0, s>>>(seed, first, count, off, arena);
     return hipGetLastError();
 }
 

@@ -214,6 +214,14 @@ class Engine:
     def synth_requests_device(self, seed: int, first: int, count: int, data_len: int, d_arena: int) -> None:
         self._check(self._lib.mirsha_synth_requests_device(self.ctx, seed, first, count, data_len, d_arena))
 
+    def synth_mixed_lengths_device(self, seed: int, first: int, count: int, d_len: int) -> None:
+        """Config-5 message lengths (u32) of requests [first, first + count) into d_len."""
+        self._check(self._lib.mirsha_synth_mixed_lengths_device(self.ctx, seed, first, count, d_len))
+
+    def synth_mixed_device(self, seed: int, first: int, count: int, d_off: int, d_arena: int) -> None:
+        """Config-5 message bytes of requests [first, first + count) at d_arena + d_off[r]."""
+        self._check(self._lib.mirsha_synth_mixed_device(self.ctx, seed, first, count, d_off, d_arena))
+
 
 class Pipeline:
     """mirsha_pipeline: a request -> batch-digest plan reused across runs of one

@@ -56,3 +56,42 @@ def batch_lists(n_req: int, batch_size: int, first_req: int = 0) -> tuple[np.nda
     idx = np.arange(n_req, dtype=np.uint32)
     first = np.minimum(np.arange(n_b + 1, dtype=np.int64) * batch_size, n_req).astype(np.uint32)
     return idx, first
+
+
+# One device launch addresses at most MIRSHA_MAX_DEVICE_ARENA_BYTES of arena
+# (32-bit buffer offsets, include/mirsha.h); larger device-resident streams
+# (BASELINE config 5: ~123 GB of mixed-size requests per GPU) are hashed in
+# contiguous origin-order windows, each with its own length-bucketed order.
+MAX_WINDOW_BYTES = 0xFFFFFF00
+
+
+def arena_windows(off, length, max_bytes: int = MAX_WINDOW_BYTES) -> list[tuple[int, int, int]]:
+    """Split requests (origin order, ascending offsets) into windows [i0, i1)
+    whose bytes [off[i0], off[i1-1] + len[i1-1]) span at most max_bytes.
+    Returns (i0, i1, base) with base = off[i0]."""
+    off = np.asarray(off, dtype=np.uint64)
+    ln = np.asarray(length, dtype=np.uint64)
+    n = off.size
+    if n == 0:
+        return []
+    end = off + ln
+    if np.any(ln > max_bytes):
+        raise ValueError("a single message exceeds the window size")
+    out = []
+    i0 = 0
+    while i0 < n:
+        base = int(off[i0])
+        # last request whose end fits in [base, base + max_bytes]
+        i1 = int(np.searchsorted(end, base + max_bytes, side="right"))
+        i1 = max(i1, i0 + 1)
+        out.append((i0, i1, base))
+        i0 = i1
+    return out
+
+
+def window_orders(length, windows) -> np.ndarray:
+    """Concatenated per-window processing orders (indices relative to the
+    window start), each longest-first by block count, stable (mirsha_bucket_order)."""
+    blk = blocks_for_len(length).astype(np.int64)
+    parts = [np.argsort(-blk[i0:i1], kind="stable").astype(np.uint32) for i0, i1, _ in windows]
+    return np.concatenate(parts) if parts else np.zeros(0, dtype=np.uint32)

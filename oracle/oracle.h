@@ -85,6 +85,19 @@ uint64_t oracle_splitmix64(uint64_t x);
 void oracle_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
                          uint8_t* arena);
 
+/* BASELINE config 5 (mixed sizes): request i's data length is
+ * log-uniform over the octaves of [64, 65536) and uniform inside an octave,
+ * in integer arithmetic (bit-identical on host, device and numpy):
+ *   x = splitmix64(seed ^ i ^ ORACLE_LEN_TAG) >> 40;  t = 10 x;
+ *   e = t >> 24;  m = t & 0xFFFFFF;  data_len = (64 << e) + (((64 << e) * m) >> 24).
+ * Message = LE64(i % 16) || LE64(i / 16) || data (bytes as oracle_gen_requests). */
+#define ORACLE_LEN_TAG 0x4C454E4754480000ull
+uint32_t oracle_mixed_data_len(uint64_t seed, uint64_t i);
+/* Messages for the request ids[k] (any order), packed densely in that order:
+ * off_out[k] / len_out[k] = offset / message length (16 + data_len) of ids[k]. */
+void oracle_gen_mixed(uint64_t seed, const uint64_t* ids, uint64_t n, uint8_t* arena, uint64_t* off_out,
+                      uint32_t* len_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -297,3 +297,30 @@ void oracle_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t
         }
     }
 }
+
+uint32_t oracle_mixed_data_len(uint64_t seed, uint64_t i) {
+    const uint64_t x = oracle_splitmix64(seed ^ i ^ ORACLE_LEN_TAG) >> 40;
+    const uint64_t t = 10u * x;
+    const uint64_t e = t >> 24, m = t & 0xFFFFFFu;
+    return (uint32_t)((64ull << e) + (((64ull << e) * m) >> 24));
+}
+
+void oracle_gen_mixed(uint64_t seed, const uint64_t* ids, uint64_t n, uint8_t* arena, uint64_t* off_out,
+                      uint32_t* len_out) {
+    uint64_t p = 0;
+    for (uint64_t k = 0; k < n; k++) {
+        const uint64_t i = ids[k];
+        const uint32_t dl = oracle_mixed_data_len(seed, i);
+        uint8_t* m = arena + p;
+        oracle_le64(i % 16, m);
+        oracle_le64(i / 16, m + 8);
+        const uint64_t key = oracle_splitmix64(seed ^ i);
+        for (uint32_t j = 0; j * 8 < dl; j++) {
+            const uint64_t w = oracle_splitmix64(key + j);
+            for (uint32_t b = 0; b < 8 && j * 8 + b < dl; b++) m[16 + j * 8 + b] = (uint8_t)(w >> (8 * b));
+        }
+        off_out[k] = p;
+        len_out[k] = 16u + dl;
+        p += 16u + dl;
+    }
+}

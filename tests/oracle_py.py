@@ -37,6 +37,9 @@ def load() -> ctypes.CDLL:
     lib.oracle_gen_requests.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, vp]
     lib.oracle_sha256_force_impl.argtypes = [ctypes.c_int]
     lib.oracle_sha256_has_shani.restype = ctypes.c_int
+    lib.oracle_mixed_data_len.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
+    lib.oracle_mixed_data_len.restype = ctypes.c_uint32
+    lib.oracle_gen_mixed.argtypes = [ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp, vp]
     lib.oracle_splitmix64.argtypes = [ctypes.c_uint64]
     lib.oracle_splitmix64.restype = ctypes.c_uint64
     _lib = lib
@@ -87,6 +90,24 @@ def gen_requests(seed: int, first: int, count: int, data_len: int) -> np.ndarray
     out = np.empty(count * (16 + data_len), dtype=np.uint8)
     lib.oracle_gen_requests(seed, first, count, data_len, _p(out))
     return out
+
+
+def mixed_data_len(seed: int, i: int) -> int:
+    """BASELINE config 5 data length of request i (oracle.h, oracle_mixed_data_len)."""
+    return int(load().oracle_mixed_data_len(seed, i))
+
+
+def gen_mixed(seed: int, ids) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Config-5 messages of the request ids (any order), packed densely: (arena, off, len)."""
+    lib = load()
+    ids = np.ascontiguousarray(ids, dtype=np.uint64)
+    total = int(sum(16 + lib.oracle_mixed_data_len(seed, int(i)) for i in ids))
+    arena = np.empty(max(total, 1), dtype=np.uint8)
+    off = np.empty(ids.size, dtype=np.uint64)
+    ln = np.empty(ids.size, dtype=np.uint32)
+    if ids.size:
+        lib.oracle_gen_mixed(seed, _p(ids), ids.size, _p(arena), _p(off), _p(ln))
+    return arena[:total], off, ln
 
 
 def force_impl(impl: int) -> None:

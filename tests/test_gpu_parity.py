@@ -517,3 +517,44 @@ def test_fused_plans_interleaved(engine):
             assert np.array_equal(lst, oracle_py.batch_digests(want_req, idx, first))
     pa.close()
     pb.close()
+
+
+def test_config5_generator_and_wide_arena(engine):
+    """Config-5 mixed-size generator (device) vs the oracle, and the 64-bit
+    addressed loader on an arena > 4 GiB: messages packed at the start, past
+    4 GiB, and ending exactly at arena_len (range-checked tail)."""
+    torch = _torch()
+    seed, first, n = synth.SEED_BASE + 5, 10**7 + 3, 1500
+    d_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    engine.synth_mixed_lengths_device(seed, first, n, d_len.data_ptr())
+    engine.sync()
+    ln = d_len.cpu().numpy().view(np.uint32)
+    arena_o, off_o, ln_o = oracle_py.gen_mixed(seed, np.arange(first, first + n, dtype=np.uint64))
+    assert np.array_equal(ln, ln_o)
+    # first half packed from 0 (odd start), second half packed to end exactly at arena_len > 4 GiB
+    half = n // 2
+    off = np.zeros(n, dtype=np.uint64)
+    off[:half] = 3 + np.concatenate([[0], np.cumsum(ln[:half - 1], dtype=np.uint64)])
+    tail = int(ln[half:].sum())
+    arena_len = (1 << 32) + 12345 + tail
+    off[half:] = arena_len - tail + np.concatenate([[0], np.cumsum(ln[half:-1], dtype=np.uint64)])
+    d_arena = torch.zeros(arena_len, dtype=torch.uint8, device="cuda")
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    engine.synth_mixed_device(seed, first, n, d_off.data_ptr(), d_arena.data_ptr())
+    engine.sync()
+    # bytes of a few messages vs the oracle
+    for k in (0, 1, half - 1, half, n - 1):
+        got = d_arena[int(off[k]):int(off[k]) + int(ln[k])].cpu().numpy()
+        want = arena_o[int(off_o[k]):int(off_o[k]) + int(ln_o[k])]
+        assert np.array_equal(got, want), k
+    want = oracle_py.hash_requests(arena_o, off_o, ln_o)
+    from mirbft_amd import bucket_order
+
+    order, _ = bucket_order(ln)
+    d_out = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
+    for d_order in (None, torch.from_numpy(order.view(np.int32)).cuda()):
+        d_out.zero_()
+        engine.hash_batch_device(d_arena.data_ptr(), arena_len, d_off.data_ptr(), d_len.data_ptr(),
+                                 None if d_order is None else d_order.data_ptr(), n, d_out.data_ptr())
+        engine.sync()
+        assert np.array_equal(d_out.cpu().numpy(), want)

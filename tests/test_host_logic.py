@@ -56,3 +56,21 @@ def test_batch_lists():
     idx, first = sharding.batch_lists(45, 20)
     assert first.tolist() == [0, 20, 40, 45]
     assert idx.tolist() == list(range(45))
+
+
+def test_arena_windows_cover_and_bound():
+    rng = np.random.default_rng(3)
+    ln = rng.integers(16, 70000, 5000).astype(np.uint64)
+    off = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+    cap = 10_000_000
+    wins = sharding.arena_windows(off, ln, cap)
+    assert wins[0][0] == 0 and wins[-1][1] == ln.size
+    for (a0, a1, base), (b0, _, _) in zip(wins, wins[1:] + [(ln.size, None, None)]):
+        assert a1 == b0 and base == off[a0]
+        assert int(off[a1 - 1] + ln[a1 - 1]) - base <= cap
+    order = sharding.window_orders(ln, wins)
+    for i0, i1, _ in wins:
+        o = order[i0:i1]
+        assert sorted(o.tolist()) == list(range(i1 - i0))
+        blk = sharding.blocks_for_len(ln[i0:i1][o]).astype(np.int64)
+        assert np.all(np.diff(blk) <= 0)
