@@ -20,6 +20,15 @@ Per round (14 VALU ops; + 10 for a schedule word when j >= 16):
   h  += S0 + maj            (new a)                             1
 Schedule: W[j] += s1(W[j-2]) + s0(W[j-15]) + W[j-7]   (2 alignbit + 1 shift + bitop3) x 2 + add3 + add
 
+Issue yield after every 4-cycle-class op (rounds_asm): a `s_nop 0` after each
+v_alignbit_b32 / v_add3_u32 lets the SIMD's age-ordered VALU arbiter pass to
+another wave instead of waiting on this one's next instruction.  Measured on
+the pure-register compression loop (tools/compress_bench.hip,
+profiles/r01/compress_variants.jsonl): 5,498 -> 5,021 cycles per
+wave-compression at 8 waves/SIMD (-8.7 %), 5,562 -> 5,097 at 4; a v_mov_b32
+filler gives nearly the same (5,041), two fillers or `s_nop 1` lose, and a
+filler after the 2-cycle-class ops loses.
+
 Run:  python gen_rounds_asm.py > sha256_rounds_asm.h
 """
 
@@ -45,7 +54,19 @@ def op(i):
     return f"%{i}"
 
 
-def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr"):
+COMPLEX = ("v_alignbit_b32", "v_add3_u32", "v_bfi_b32")
+
+
+def yield_after_complex(lines):
+    out = []
+    for ln in lines:
+        out.append(ln)
+        if ln.split()[0] in COMPLEX:
+            out.append("s_nop 0")
+    return out
+
+
+def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr", nops=False):
     lines = []
     for r in range(8):
         j = j0 + r
@@ -99,7 +120,7 @@ def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr"):
             lines.append(f"v_add3_u32 {h}, {h}, {t0}, {t1}")
         else:
             lines += [f"v_add_u32_e32 {h}, {h}, {t0}", f"v_add_u32_e32 {h}, {h}, {t1}"]
-    return lines
+    return yield_after_complex(lines) if nops else lines
 
 
 def block_ilp(j0):
@@ -168,20 +189,21 @@ def emit_fn_ilp(name):
 
 
 VARIANTS = {
-    # name: (ch_mode, add_mode, k_mode)
-    "rounds_asm": ("bitop3", "add3", "sgpr"),
-    "rounds_asm_bfi": ("bfi", "add3", "sgpr"),
-    "rounds_asm_add2": ("bitop3", "add", "sgpr"),
-    "rounds_asm_lit": ("bitop3", "add3", "lit"),
-    "rounds_asm_add2lit": ("bitop3", "add", "lit"),
+    # name: (ch_mode, add_mode, k_mode, nops)
+    "rounds_asm": ("bitop3", "add3", "sgpr", True),
+    "rounds_asm_nonop": ("bitop3", "add3", "sgpr", False),
+    "rounds_asm_bfi": ("bfi", "add3", "sgpr", False),
+    "rounds_asm_add2": ("bitop3", "add", "sgpr", False),
+    "rounds_asm_lit": ("bitop3", "add3", "lit", False),
+    "rounds_asm_add2lit": ("bitop3", "add", "lit", False),
 }
 
 
-def emit_fn(name, ch_mode, add_mode, k_mode):
+def emit_fn(name, ch_mode, add_mode, k_mode, nops):
     out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16]) {{",
            "    uint32_t t0, t1, t2, t3;"]
     for j0 in range(0, 64, 8):
-        body = block(j0, ch_mode, add_mode, k_mode)
+        body = block(j0, ch_mode, add_mode, k_mode, nops)
         out.append(f"    // rounds {j0}..{j0 + 7}")
         out.append("    asm volatile(")
         for ln in body:
@@ -212,8 +234,8 @@ def emit():
     out.append("")
     out.append("// s[0..7] = working variables a..h (updated in place: after 8 rounds the")
     out.append("// names have rotated back), w[0..15] = schedule window (consumed).")
-    for name, (ch, ad, km) in VARIANTS.items():
-        out += emit_fn(name, ch, ad, km)
+    for name, (ch, ad, km, nops) in VARIANTS.items():
+        out += emit_fn(name, ch, ad, km, nops)
     out.append("// Latency-oriented order (lone waves): same instructions, 12 temporaries.")
     out += emit_fn_ilp("rounds_asm_ilp")
     out.append("}  // namespace mirsha")

@@ -339,7 +339,7 @@ __device__ __forceinline__ bool hash_list(__amdgpu_buffer_rsrc_t drs, __amdgpu_b
                 w[14] = L >> 29;
                 w[15] = L << 3;
             }
-            compress_asm(st, w);
+            compress_asm_lat(st, w);
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) cur[i] = nxt[i];
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
                 w[14] = L >> 29;
                 w[15] = L << 3;
             }
-            compress_asm(st, w);
+            compress_asm_lat(st, w);
         }
 #pragma unroll
         for (int i = 0; i < 4; i++) cur[i] = nxt[i];
@@ -612,7 +612,7 @@ __device__ __forceinline__ void fused_list_group_deep(const FusedArgs& a, __amdg
                     w[14] = L >> 29;
                     w[15] = L << 3;
                 }
-                compress_asm(st, w);
+                compress_asm_lat(st, w);
             }
         }
         stamp(2u * a.n_tiles + a.n_counters + a.n_groups + cb + chunk);
@@ -668,7 +668,7 @@ __device__ __forceinline__ void hash_tile_deep(const uint8_t* __restrict__ arena
         const uint32_t nbk = blk + (uint32_t)kTileDepth;
 #pragma unroll
         for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, nbk, (uint32_t)q, nbk < nb, rc[kTileDepth - 1][q]);
-        if (blk < nb) compress_asm(st, w);
+        if (blk < nb) compress_asm_lat(st, w);
     }
     if (valid) store_digest_sc1(ors, msg, st);
 }

@@ -73,12 +73,24 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
 
 // The same compression with the 64 rounds in generated gfx950 assembly
 // (sha256_rounds_asm.h): a..h + W[16] + 4 temporaries, no compiler-hoisted
-// schedule partial sums.
+// schedule partial sums.  Throughput form: an issue-yield `s_nop 0` after
+// every 4-cycle-class op (-8.7 % cycles at 4-8 waves/SIMD, gen_rounds_asm.py).
 __device__ __forceinline__ void compress_asm(uint32_t st[8], uint32_t w[16]) {
     uint32_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = st[i];
     rounds_asm(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] += s[i];
+}
+
+// Latency form (no yields) for digest-list chains, which run at most one
+// wave per SIMD: there the yields only lengthen the chain.
+__device__ __forceinline__ void compress_asm_lat(uint32_t st[8], uint32_t w[16]) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = st[i];
+    rounds_asm_nonop(s, w);
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] += s[i];
 }
