@@ -12,6 +12,13 @@ Other configs (--config): 3 = 2^18 x 4 KB requests + BatchSize-500
 VerifyBatch digests (batch_tracker.go:147-150); 5 = mixed 64 B - 64 KB
 requests (log-uniform octaves), 12.5M per GPU = 10^8 over 8 GPUs.
 Inputs are generated on device and resident in HBM before the timed region.
+4 = one node's Ready() cycle during a 64-node epoch change: 4096
+EpochChangeAck hash requests (64 origins x 64 relaying sources, 61.6 KB
+epochChangeHashData payloads of 3847 slices each, stateless.go:311-340) given
+as HOST slices, as the Go state machine hands them over; each step is the
+host API call (dedup + pack + H2D + kernel + D2H), so this config is
+PCIe-inclusive by nature.  A synthetic stand-in: the testengine run that
+BASELINE config 4 names needs Go, which this image lacks.
 
 Multi-GPU: one process per GPU (torchrun); every rank hashes its own request
 range (weak scaling), no collective in the data path; the barrier and
@@ -49,6 +56,8 @@ CONFIGS = {
     3: (4096, 1 << 18, 500, "Large-payload stream: 256K requests x 4 KB, BatchSize 500, VerifyBatch recomputation"),
     5: (None, 12_500_000, 0, "Mixed-size stream: 64 B - 64 KB requests (log-uniform octaves), "
                              "12.5M per GPU (10^8 over 8 GPUs), request-range sharded"),
+    4: (None, 4096, 0, "Epoch-change cycle of a 64-node network: 64 origins x 64 relaying sources "
+                       "EpochChangeAck digests (61.6 KB payloads, host slices), content-addressed dedup"),
 }
 
 
@@ -64,10 +73,12 @@ def parse():
                    help="untimed steps; MI355X needs ~20+ ms of sustained load to reach its working clock")
     p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
-    p.add_argument("--variant", type=int, default=0, help="0 = LDS-staged loader, 1 = direct per-lane loads")
+    p.add_argument("--variant", type=int, default=0, help="0 = LDS-staged loader (low-occupancy kernel for <= 1 wave/SIMD launches), "
+                        "1 = direct per-lane loads, 2/3 = C++ rounds, 4 = low-occupancy kernel, 5 = LDS kernel only")
     p.add_argument("--windows", action="store_true",
                    help="config 5: hash in <= 4 GiB windows (one launch each) instead of one 64-bit-addressed launch")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline sample (0 disables)")
+    p.add_argument("--dedup", type=int, default=1, help="config 4: 1 = mirsha_hash_slices_dedup, 0 = plain")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-API measurement")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential", "streams"],
@@ -333,6 +344,90 @@ class MixedWorkload:
         return {}
 
 
+class EpochChangeWorkload:
+    """Config 4 (see the module docstring): host-slice requests through the
+    host API, with content-addressed dedup (mirsha_hash_slices_dedup)."""
+
+    N_NODES, N_CP, N_P, N_Q = 64, 3, 640, 640
+    data_note = "synthetic epochChangeHashData payloads (numpy, host memory), one copy per ack"
+
+    def __init__(self, a, eng, dev, rank):
+        from mirbft_amd import SliceArrays, hashdata
+
+        self.a, self.eng = a, eng
+        _, n0, _, self.desc = CONFIGS[4]
+        self.n = n = a.requests or n0
+        self.dedup = bool(a.dedup)
+        self.buf, so, sl, self.first, self.origin = hashdata.epoch_change_cycle(
+            self.N_NODES, n, self.N_CP, self.N_P, self.N_Q, new_epoch=2 + rank)
+        self.sl = SliceArrays.from_buffer(self.buf, so, sl, self.first)
+        self.plen = self.buf.size // n
+        self.slices_per_req = int(self.first[1])
+        self.bytes_hashed = self.buf.size
+        self.digests = n
+        self.distinct = min(n, self.N_NODES)
+        self.hashed_reqs = self.distinct if self.dedup else n
+        self.req_blocks = int(blocks(self.plen)) * self.hashed_reqs
+        self.plan = None
+        eng.set_stream(None)  # host API on the engine's own stream
+
+    def step(self):
+        self.eng.hash_slice_arrays(self.sl, dedup=self.dedup)
+
+    def after(self):
+        pass
+
+    def dominant(self):
+        n_m, ms_m = self.eng.kernel_time(KERNEL_MSGS)
+        return "sha256_msgs_kernel", n_m, ms_m, self.req_blocks, self.hashed_reqs * (self.plen + 32)
+
+    def self_check(self):
+        import hashlib
+
+        got = self.eng.hash_slice_arrays(self.sl, dedup=self.dedup)
+        ok = self.eng.last_unique == self.hashed_reqs
+        for r in list(range(0, self.n, max(1, self.n // 16))) + [self.n - 1]:
+            want = hashlib.sha256(self.buf[r * self.plen:(r + 1) * self.plen].tobytes()).digest()
+            ok &= got[r].tobytes() == want
+        return bool(ok)
+
+    def pcie(self):
+        other = not self.dedup
+        reps, t0 = 5, time.perf_counter()
+        for _ in range(reps):
+            self.eng.hash_slice_arrays(self.sl, dedup=other)
+        dt = (time.perf_counter() - t0) / reps
+        return {"dedup": other, "digests_per_s": self.n / dt, "ms_per_call": dt * 1e3,
+                "note": "the same cycle with dedup toggled (A/B)"}
+
+    def cpu_baseline(self, seconds):
+        o = _oracle()
+        k = min(self.n, 256)  # 256 x 61.6 KB = 15.8 MB of the same requests
+        arena = self.buf[: k * self.plen]
+        off = np.arange(k, dtype=np.uint64) * self.plen
+        ln = np.full(k, self.plen, dtype=np.uint32)
+        res = _time_cpu(lambda t: o.hash_requests(arena, off, ln, threads=t), seconds,
+                        (1, min(16, os.cpu_count() or 1)))
+        done1, dt1 = res[1]
+        tp = max(res)
+        return {
+            "value": done1 * k / dt1, "unit": "digests/s", "cores": 1, "kind": "port",
+            "sample": f"{done1} passes x {k} EpochChangeAck requests x {self.plen} B, {dt1:.1f} s, oracle C port "
+                      f"of processor.go:133-143 (every ack hashed, as the reference does), SHA-NI compression",
+            "pool": {"value": res[tp][0] * k / res[tp][1], "threads": tp},
+            "cpu": _cpu_model(),
+        }
+
+    def config_fields(self):
+        return {"requests_per_gpu": self.n, "payload_bytes": self.plen, "slices_per_request": self.slices_per_req,
+                "origins": self.N_NODES, "distinct_payloads": self.distinct, "dedup": self.dedup,
+                "input": "host slices (Go-side [][]byte); each step = pack + H2D + kernel + D2H",
+                "compressions_per_step_per_gpu": self.req_blocks}
+
+    def extra(self):
+        return {"pcie_inclusive_by_design": True}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -353,7 +448,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
 
-    wl = (MixedWorkload if a.config == 5 else BatchWorkload)(a, eng, dev, rank)
+    wl = {5: MixedWorkload, 4: EpochChangeWorkload}.get(a.config, BatchWorkload)(a, eng, dev, rank)
     torch.cuda.synchronize(dev)
 
     for _ in range(a.warmup):
@@ -420,12 +515,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (splitmix64 request stream generated on device, SURVEY.md §8d)",
+            "data": getattr(wl, "data_note", "synthetic (splitmix64 request stream generated on device, SURVEY.md §8d)"),
             "config": {
                 "workload": f"config{a.config}: {wl.desc}",
                 **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx"][a.variant],
+                "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only"][a.variant],
             },
             "gb_per_s_hashed": gbps,
             "roofline": {

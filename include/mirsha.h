@@ -72,9 +72,12 @@ int mirsha_ctx_set_stream(mirsha_ctx* ctx, void* hip_stream);
 void* mirsha_ctx_stream(mirsha_ctx* ctx);
 
 /* Kernel variant for sha256 over packed messages (A/B measurement):
- * 0 = LDS-staged coalesced loader + generated-asm rounds (default),
+ * 0 = LDS-staged coalesced loader + generated-asm rounds (default; a launch
+ *     of at most 1024 waves -- one per SIMD -- takes the low-occupancy kernel:
+ *     prefetching direct loads, no-yield rounds),
  * 1 = direct per-lane loads + asm rounds, 2 = LDS loader + compiler-scheduled
- * C++ rounds, 3 = direct loads + C++ rounds.  All are bit-exact. */
+ * C++ rounds, 3 = direct loads + C++ rounds, 4 = the low-occupancy kernel at
+ * any size, 5 = the LDS kernel at any size.  All are bit-exact. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
 /* Per-kernel device-time accounting with HIP events on the launch stream.
@@ -105,6 +108,50 @@ int mirsha_hash_batch(mirsha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
 int mirsha_hash_slices(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
                        const uint64_t* slice_len, const uint32_t* slice_first, uint32_t n,
                        uint8_t* digests_out);
+
+/* Content-addressed dedup of one Ready() cycle.  During an
+ * epoch change every node hashes the same EpochChange payload once per
+ * acknowledging source (applyEpochChangeAckMsg, epoch_target.go:459-477, with
+ * epochChangeHashData, stateless.go:311-340): N sources x N origins requests,
+ * N distinct payloads.  Requests whose concatenated bytes are equal are hashed
+ * ONCE; every duplicate still gets its own digest at digests_out[32*i], in
+ * origin order (equality is confirmed byte for byte; the fingerprint only
+ * groups candidates).  *n_unique_out (may be NULL) = distinct requests hashed.
+ * At most MIRSHA_MAX_DEVICE_ARENA_BYTES of distinct bytes per call. */
+int mirsha_hash_slices_dedup(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
+                             const uint64_t* slice_len, const uint32_t* slice_first, uint32_t n,
+                             uint8_t* digests_out, uint32_t* n_unique_out);
+
+/* Host-only (no device, no context): the dedup plan the call above uses.
+ * rep_out[i] = smallest j <= i whose request bytes equal request i's
+ * (rep_out[i] == i for the first of each distinct content). */
+int mirsha_dedup_plan(const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                      const uint32_t* slice_first, uint32_t n, uint32_t* rep_out,
+                      uint32_t* n_unique_out);
+
+/* ---------------------------------------- asynchronous, order-preserving */
+/* Replaces the hash stage of ProcessorWorkPool (processor.go:312-361,
+ * 447-470) without its completion-order output: the caller
+ * submits a Ready() cycle's requests, goes on with the WAL writes and network
+ * sends the cycle also carries (actions.go:22-23 lets hashing run beside
+ * them), then waits for the digests.
+ *   mirsha_submit_slices packs the requests into the context's pinned staging
+ *     before it returns (the caller may reuse the slices at once), queues the
+ *     H2D copy, the kernel and the D2H copy, and returns a ticket (> 0).
+ *     digests_out must stay valid until that ticket is waited for: the
+ *     digests land there, in origin order, inside mirsha_wait / mirsha_poll.
+ *     flags: 0 or MIRSHA_SUBMIT_DEDUP.  Up to 4 submissions are in flight;
+ *     a fifth first retires the oldest.
+ *   mirsha_wait blocks until every submission up to `ticket` is complete and
+ *     its digests are written (submissions complete in submission order).
+ *   mirsha_poll sets *done = 1 (and writes the digests) if every submission
+ *     up to `ticket` is complete, else 0 without blocking. */
+#define MIRSHA_SUBMIT_DEDUP 1
+int mirsha_submit_slices(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
+                         const uint64_t* slice_len, const uint32_t* slice_first, uint32_t n,
+                         uint8_t* digests_out, int flags, uint64_t* ticket_out);
+int mirsha_wait(mirsha_ctx* ctx, uint64_t ticket);
+int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
 
 /* Request digests, then the dependent batch digests computed ON DEVICE from
  * the device-resident request digests (no host round trip):

@@ -21,6 +21,7 @@ MIRSHA_ENOMEM = -3
 MIRSHA_ERANGE = -4
 MIRSHA_ENODEV = -5
 MIRSHA_NULL_INDEX = 0xFFFFFFFF
+MIRSHA_SUBMIT_DEDUP = 1
 
 ERROR_NAMES = {
     MIRSHA_EINVAL: "EINVAL",
@@ -49,6 +50,11 @@ SIGNATURES = {
     "mirsha_sync": (c_int, [c_void_p]),
     "mirsha_hash_batch": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p]),
     "mirsha_hash_slices": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
+    "mirsha_hash_slices_dedup": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, _u32p]),
+    "mirsha_dedup_plan": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, _u32p]),
+    "mirsha_submit_slices": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_int, _u64p]),
+    "mirsha_wait": (c_int, [c_void_p, c_uint64]),
+    "mirsha_poll": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
     "mirsha_hash_requests_then_batches": (
         c_int,
         [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p],

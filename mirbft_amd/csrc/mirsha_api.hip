@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "../../include/mirsha.h"
+#include "mirsha_host.h"
 #include "mirsha_kernels.h"
 #include "sha256_device.h"
 
@@ -67,6 +68,22 @@ struct PinnedBuf {
     void release() { if (p) (void)hipHostFree(p); p = nullptr; cap = 0; }
 };
 
+// One in-flight submission of the asynchronous API (mirsha_submit_slices):
+// its own pinned staging and device buffers, so up to kAsyncSlots Ready()
+// cycles can be packed / copied / hashed while the caller works on.
+constexpr uint32_t kAsyncSlots = 4;
+struct AsyncSlot {
+    PinnedBuf stage;  // [arena bytes | off u64[m] | len u32[m] | order u32[m]]
+    PinnedBuf dig;    // m x 32 digests (D2H target)
+    DevBuf dev;       // the same layout as stage, then m x 32 digests
+    hipEvent_t done = nullptr;
+    uint64_t ticket = 0;
+    bool busy = false;
+    uint8_t* user_out = nullptr;
+    uint32_t n = 0, m = 0;
+    std::vector<uint32_t> rank;  // request -> row of `dig` (empty: identity)
+};
+
 struct KernelTimer {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     std::vector<hipEvent_t> pool;
@@ -87,6 +104,9 @@ struct mirsha_ctx {
     PinnedBuf h_stage;
     KernelTimer timers[5];         // msgs, lists, gen, chain, fused
     hipStream_t chain_stream = nullptr;  // dependent-pass stream of the pipeline (lazy)
+    AsyncSlot slots[kAsyncSlots];
+    uint64_t next_ticket = 1;  // ticket of the next submission
+    uint64_t done_ticket = 0;  // every ticket <= this one has completed
 };
 
 // A request -> batch-digest pipeline plan (see mirsha.h, mirsha_pipeline_create).
@@ -711,6 +731,144 @@ void pipeline_free(mirsha_pipeline* p) {
     p->d_trace.release();
 }
 
+
+// Validates a slice-list request set and returns each request's total length.
+int slice_lengths(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                  const uint32_t* slice_first, uint32_t n, const uint8_t* out, std::vector<uint32_t>& len) {
+    if (!slice_first || !out) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (slice_first[0] != 0) return fail(c, MIRSHA_EINVAL, "slice_first[0] must be 0");
+    const uint32_t ns = slice_first[n];
+    if (ns && (!slice_ptr || !slice_len)) return fail(c, MIRSHA_EINVAL, "NULL slice arrays");
+    len.resize(n);
+    // err[i]: 0 ok, 1 not monotone, 2 NULL slice, 3 too long (first error reported)
+    std::vector<uint8_t> err(n, 0);
+    const uint64_t meta = 16ull * (ns > slice_first[0] ? ns : 0u);
+    mirsha::host::parallel_for(n, mirsha::host::threads_for(meta, n), [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; i++) {
+            if (slice_first[i + 1] < slice_first[i] || slice_first[i + 1] > ns) { err[i] = 1; continue; }
+            uint64_t L = 0;
+            for (uint32_t s = slice_first[i]; s < slice_first[i + 1]; s++) {
+                if (slice_len[s] && !slice_ptr[s]) { err[i] = 2; break; }
+                L += slice_len[s];
+            }
+            if (!err[i] && L > MIRSHA_MAX_MESSAGE_BYTES) err[i] = 3;
+            len[i] = (uint32_t)L;
+        }
+    });
+    for (uint32_t i = 0; i < n; i++) {
+        if (err[i] == 1) return fail(c, MIRSHA_EINVAL, "slice_first not monotone at request %u", i);
+        if (err[i] == 2) return fail(c, MIRSHA_EINVAL, "request %u has a NULL slice", i);
+        if (err[i] == 3) return fail(c, MIRSHA_ERANGE, "request %u exceeds %u bytes", i, MIRSHA_MAX_MESSAGE_BYTES);
+    }
+    return MIRSHA_OK;
+}
+
+// Copies a completed submission's digests to the caller, in origin order.
+int async_complete(mirsha_ctx* c, AsyncSlot& sl) {
+    HIP_TRY(c, hipEventSynchronize(sl.done));
+    const uint8_t* d = sl.dig.as<uint8_t>();
+    if (sl.rank.empty()) {
+        memcpy(sl.user_out, d, 32ull * sl.n);
+    } else {
+        for (uint32_t i = 0; i < sl.n; i++) memcpy(sl.user_out + 32ull * i, d + 32ull * sl.rank[i], 32);
+    }
+    sl.busy = false;
+    c->done_ticket = std::max(c->done_ticket, sl.ticket);
+    return MIRSHA_OK;
+}
+
+int async_wait_upto(mirsha_ctx* c, uint64_t ticket) {
+    for (uint64_t t = c->done_ticket + 1; t <= ticket; t++) {
+        AsyncSlot& sl = c->slots[(t - 1) % kAsyncSlots];
+        if (sl.busy && sl.ticket == t)
+            if (int rc = async_complete(c, sl)) return rc;
+    }
+    return MIRSHA_OK;
+}
+
+constexpr uint64_t align8(uint64_t x) { return (x + 7u) & ~7ull; }
+
+int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                 const uint32_t* slice_first, uint32_t n, uint8_t* out, int flags, uint64_t* ticket_out,
+                 uint32_t* n_unique_out) {
+    if (flags & ~MIRSHA_SUBMIT_DEDUP) return fail(c, MIRSHA_EINVAL, "unknown submit flags 0x%x", flags);
+    std::vector<uint32_t> len;
+    if (n) {
+        if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
+    }
+    if (int rc = use_device(c)) return rc;
+    AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
+    if (sl.busy)
+        if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
+    // Plan: which requests reach the GPU (all, or one per distinct content).
+    std::vector<uint32_t> which;  // unique request indices, ascending (empty = all)
+    sl.rank.clear();
+    uint32_t m = n;
+    if ((flags & MIRSHA_SUBMIT_DEDUP) && n > 1) {
+        std::vector<uint64_t> rl(len.begin(), len.end());
+        std::vector<uint32_t> rep(n);
+        m = mirsha::host::dedup_plan(slice_ptr, slice_len, slice_first, n, rl.data(), rep.data());
+        if (m < n) {
+            which.reserve(m);
+            sl.rank.resize(n);
+            for (uint32_t i = 0; i < n; i++) {
+                if (rep[i] == i) {
+                    sl.rank[i] = (uint32_t)which.size();
+                    which.push_back(i);
+                } else {
+                    sl.rank[i] = sl.rank[rep[i]];
+                }
+            }
+        }
+    }
+    if (n_unique_out) *n_unique_out = m;
+    std::vector<uint64_t> poff(m);
+    std::vector<uint32_t> plen(m);
+    uint64_t bytes = 0;
+    for (uint32_t k = 0; k < m; k++) {
+        const uint32_t i = which.empty() ? k : which[k];
+        poff[k] = bytes;
+        plen[k] = len[i];
+        bytes += len[i];
+    }
+    if (bytes + kArenaSlack > MIRSHA_MAX_DEVICE_ARENA_BYTES)
+        return fail(c, MIRSHA_ERANGE, "submission of %llu bytes exceeds one device arena (%u); split it",
+                    (unsigned long long)bytes, MIRSHA_MAX_DEVICE_ARENA_BYTES);
+    const uint64_t o_off = align8(bytes + kArenaSlack);
+    const uint64_t o_len = o_off + 8ull * m, o_ord = o_len + 4ull * m, o_end = align8(o_ord + 4ull * m);
+    const uint64_t o_dig = o_end;
+    HIP_TRY(c, sl.stage.ensure(o_end));
+    HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(m, 1)));
+    HIP_TRY(c, sl.dev.ensure(o_dig + 32ull * std::max<uint32_t>(m, 1)));
+    if (!sl.done) HIP_TRY(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+    uint8_t* st = sl.stage.as<uint8_t>();
+    mirsha::host::pack(slice_ptr, slice_len, slice_first, which.empty() ? nullptr : which.data(), m, poff.data(), st,
+                       mirsha::host::threads_for(bytes, m));
+    memcpy(st + o_off, poff.data(), 8ull * m);
+    memcpy(st + o_len, plen.data(), 4ull * m);
+    const bool identity = bucket_order(plen.data(), m, reinterpret_cast<uint32_t*>(st + o_ord));
+    uint8_t* dv = sl.dev.as<uint8_t>();
+    if (m) {
+        HIP_TRY(c, hipMemcpyAsync(dv, st, o_end, hipMemcpyHostToDevice, c->stream));
+        int rc = timed_launch(c, 0, [&] {
+            return mirsha::launch_msgs(dv, bytes, reinterpret_cast<const uint64_t*>(dv + o_off),
+                                       reinterpret_cast<const uint32_t*>(dv + o_len),
+                                       identity ? nullptr : reinterpret_cast<const uint32_t*>(dv + o_ord), m,
+                                       dv + o_dig, c->variant, c->stream);
+        });
+        if (rc) return rc;
+        HIP_TRY(c, hipMemcpyAsync(sl.dig.p, dv + o_dig, 32ull * m, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(c, hipEventRecord(sl.done, c->stream));
+    sl.busy = true;
+    sl.user_out = out;
+    sl.n = n;
+    sl.m = m;
+    sl.ticket = c->next_ticket++;
+    if (ticket_out) *ticket_out = sl.ticket;
+    return MIRSHA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -762,6 +920,10 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     c->d_arena.release(); c->d_off.release(); c->d_len.release(); c->d_order.release();
     c->d_out.release(); c->d_idx.release(); c->d_first.release(); c->d_out2.release(); c->d_scratch.release();
     c->h_stage.release();
+    for (auto& sl : c->slots) {
+        sl.stage.release(); sl.dig.release(); sl.dev.release();
+        if (sl.done) (void)hipEventDestroy(sl.done);
+    }
     if (c->chain_stream) (void)hipStreamDestroy(c->chain_stream);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
@@ -778,7 +940,7 @@ int mirsha_ctx_set_stream(mirsha_ctx* c, void* s) {
 void* mirsha_ctx_stream(mirsha_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
 
 int mirsha_ctx_set_variant(mirsha_ctx* c, int v) {
-    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantDirectCxx) return MIRSHA_EINVAL;
+    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantLdsOnly) return MIRSHA_EINVAL;
     c->variant = v;
     return MIRSHA_OK;
 }
@@ -839,32 +1001,17 @@ int mirsha_hash_batch(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, c
     return MIRSHA_OK;
 }
 
+
 int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
                        const uint32_t* slice_first, uint32_t n, uint8_t* out) {
     if (!c) return MIRSHA_EINVAL;
     if (n == 0) return MIRSHA_OK;
-    if (!slice_first || !out) return fail(c, MIRSHA_EINVAL, "NULL argument");
-    if (slice_first[0] != 0) return fail(c, MIRSHA_EINVAL, "slice_first[0] must be 0");
-    const uint32_t ns = slice_first[n];
-    if (ns && (!slice_ptr || !slice_len)) return fail(c, MIRSHA_EINVAL, "NULL slice arrays");
-    std::vector<uint64_t> off(n);
-    std::vector<uint32_t> len(n);
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        if (slice_first[i + 1] < slice_first[i]) return fail(c, MIRSHA_EINVAL, "slice_first not monotone");
-        uint64_t L = 0;
-        for (uint32_t s = slice_first[i]; s < slice_first[i + 1]; s++) {
-            if (slice_len[s] && !slice_ptr[s]) return fail(c, MIRSHA_EINVAL, "slice %u is NULL", s);
-            L += slice_len[s];
-        }
-        if (L > MIRSHA_MAX_MESSAGE_BYTES) return fail(c, MIRSHA_ERANGE, "request %u is %llu bytes", i, (unsigned long long)L);
-        off[i] = total;
-        len[i] = (uint32_t)L;
-        total += L;
-    }
+    std::vector<uint32_t> len;
+    if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     if (int rc = use_device(c)) return rc;
-    // One packing pass into pinned memory (the Go side's single copy), then the
-    // common path; windows bound the staging footprint.
+    // One packing pass into pinned memory (the Go side's single copy, in
+    // parallel for large cycles), then the common path; windows bound the
+    // staging footprint.
     HIP_TRY(c, c->d_out.ensure(32ull * n));
     uint32_t i = 0;
     while (i < n) {
@@ -878,11 +1025,10 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
         uint64_t p = 0;
         for (uint32_t k = i; k < j; k++) {
             poff[k - i] = p;
-            for (uint32_t s = slice_first[k]; s < slice_first[k + 1]; s++) {
-                if (slice_len[s]) memcpy(st + p, slice_ptr[s], slice_len[s]);
-                p += slice_len[s];
-            }
+            p += len[k];
         }
+        mirsha::host::pack(slice_ptr, slice_len, slice_first + i, nullptr, j - i, poff.data(), st,
+                           mirsha::host::threads_for(bytes, j - i));
         if (bytes)
             HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, st, bytes, hipMemcpyHostToDevice, c->stream));
         if (int rc = hash_resident(c, c->d_arena.as<uint8_t>(), bytes, poff.data(), len.data() + i, j - i,
@@ -892,6 +1038,51 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
     }
     HIP_TRY(c, hipMemcpyAsync(out, c->d_out.p, 32ull * n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_hash_slices_dedup(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                             const uint32_t* slice_first, uint32_t n, uint8_t* out, uint32_t* n_unique_out) {
+    if (!c) return MIRSHA_EINVAL;
+    if (n_unique_out) *n_unique_out = 0;
+    if (n == 0) return MIRSHA_OK;
+    uint64_t t = 0;
+    if (int rc = async_submit(c, slice_ptr, slice_len, slice_first, n, out, MIRSHA_SUBMIT_DEDUP, &t, n_unique_out))
+        return rc;
+    return async_wait_upto(c, t);
+}
+
+int mirsha_submit_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                         const uint32_t* slice_first, uint32_t n, uint8_t* out, int flags, uint64_t* ticket_out) {
+    if (!c || !ticket_out) return MIRSHA_EINVAL;
+    return async_submit(c, slice_ptr, slice_len, slice_first, n, out, flags, ticket_out, nullptr);
+}
+
+int mirsha_wait(mirsha_ctx* c, uint64_t ticket) {
+    if (!c) return MIRSHA_EINVAL;
+    if (ticket == 0 || ticket >= c->next_ticket) return fail(c, MIRSHA_EINVAL, "unknown ticket %llu", (unsigned long long)ticket);
+    if (ticket <= c->done_ticket) return MIRSHA_OK;
+    if (int rc = use_device(c)) return rc;
+    return async_wait_upto(c, ticket);
+}
+
+int mirsha_poll(mirsha_ctx* c, uint64_t ticket, int* done) {
+    if (!c || !done) return MIRSHA_EINVAL;
+    if (ticket == 0 || ticket >= c->next_ticket) return fail(c, MIRSHA_EINVAL, "unknown ticket %llu", (unsigned long long)ticket);
+    *done = 0;
+    if (ticket <= c->done_ticket) {
+        *done = 1;
+        return MIRSHA_OK;
+    }
+    if (int rc = use_device(c)) return rc;
+    for (uint64_t t = c->done_ticket + 1; t <= ticket; t++) {
+        AsyncSlot& sl = c->slots[(t - 1) % kAsyncSlots];
+        const hipError_t q = hipEventQuery(sl.done);
+        if (q == hipErrorNotReady) return MIRSHA_OK;
+        if (q != hipSuccess) return fail(c, MIRSHA_EHIP, "hipEventQuery: %s", hipGetErrorString(q));
+    }
+    if (int rc = async_wait_upto(c, ticket)) return rc;
+    *done = 1;
     return MIRSHA_OK;
 }
 

@@ -1,0 +1,261 @@
+// mirsha_host.cpp — host-side packing and content-addressed dedup for the
+// C-ABI (see mirsha_host.h).  Pure CPU code: no HIP calls, so the dedup plan
+// is testable without a GPU (mirsha_dedup_plan, tests/test_host_dedup.py).
+#include "mirsha_host.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mirsha.h"
+
+namespace mirsha {
+namespace host {
+
+namespace {
+
+int env_threads() {
+    static const int v = [] {
+        const char* e = getenv("MIRSHA_HOST_THREADS");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+bool weak_fp() {
+    static const bool v = [] {
+        const char* e = getenv("MIRSHA_DEDUP_WEAK_FP");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
+inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+// Streaming word hash with a byte carry, so slicing does not matter.
+struct Fp {
+    uint64_t h0 = 0x6D69726274667030ull, h1 = 0x9E3779B97F4A7C15ull;
+    uint64_t carry = 0, total = 0;
+    int nc = 0;
+    uint64_t parity = 0;
+    inline void word(uint64_t w) {
+        // two interleaved lanes (word parity) keep the multiply chains short
+        if (parity++ & 1) {
+            h1 = rotl(h1 ^ (w * 0xBF58476D1CE4E5B9ull), 29) * 0x94D049BB133111EBull;
+        } else {
+            h0 = rotl(h0 ^ (w * 0x94D049BB133111EBull), 31) * 0xBF58476D1CE4E5B9ull;
+        }
+    }
+    void bytes(const uint8_t* p, uint64_t n) {
+        total += n;
+        while (nc && n) {
+            carry |= (uint64_t)*p++ << (8 * nc);
+            n--;
+            if (++nc == 8) { word(carry); carry = 0; nc = 0; }
+        }
+        if ((parity & 1) && n >= 8) {  // realign so word k always feeds lane k & 1
+            uint64_t a;
+            memcpy(&a, p, 8);
+            word(a);
+            p += 8;
+            n -= 8;
+        }
+        while (n >= 16) {  // = word(a); word(b) from an even parity
+            uint64_t a, b;
+            memcpy(&a, p, 8);
+            memcpy(&b, p + 8, 8);
+            h0 = rotl(h0 ^ (a * 0x94D049BB133111EBull), 31) * 0xBF58476D1CE4E5B9ull;
+            h1 = rotl(h1 ^ (b * 0xBF58476D1CE4E5B9ull), 29) * 0x94D049BB133111EBull;
+            parity += 2;
+            p += 16;
+            n -= 16;
+        }
+        while (n >= 8) {
+            uint64_t a;
+            memcpy(&a, p, 8);
+            word(a);
+            p += 8;
+            n -= 8;
+        }
+        while (n) {
+            carry |= (uint64_t)*p++ << (8 * nc);
+            nc++;
+            n--;
+        }
+    }
+    uint64_t final() {
+        if (nc) word(carry ^ ((uint64_t)nc << 56));
+        uint64_t h = h0 ^ rotl(h1, 17) ^ total * 0xD6E8FEB86659FD93ull;
+        h ^= h >> 32;
+        h *= 0xD6E8FEB86659FD93ull;
+        h ^= h >> 29;
+        return h;
+    }
+};
+
+}  // namespace
+
+int threads_for(uint64_t bytes, uint32_t n) {
+    if (n < 2 || bytes < (4ull << 20)) return 1;
+    int t = env_threads();
+    if (t <= 0) {
+        t = (int)std::thread::hardware_concurrency();
+        t = std::min(std::max(t, 1), 16);
+    }
+    const uint64_t by_bytes = bytes / (1ull << 20);  // >= 1 MiB per thread
+    t = (int)std::min<uint64_t>((uint64_t)t, std::max<uint64_t>(1, by_bytes));
+    return std::min<int>(t, (int)n);
+}
+
+void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, uint32_t)>& fn) {
+    if (n == 0) return;
+    if (threads <= 1) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(threads - 1);
+    const uint32_t step = (n + threads - 1) / threads;
+    for (int t = 1; t < threads; t++) {
+        const uint32_t lo = std::min<uint64_t>((uint64_t)t * step, n), hi = std::min<uint64_t>((uint64_t)(t + 1) * step, n);
+        if (lo < hi) pool.emplace_back([&fn, lo, hi] { fn(lo, hi); });
+    }
+    fn(0, std::min(step, n));
+    for (auto& th : pool) th.join();
+}
+
+uint64_t fingerprint(const uint8_t* const* ptr, const uint64_t* len, uint32_t s0, uint32_t s1) {
+    if (weak_fp()) return 0;
+    Fp f;
+    for (uint32_t s = s0; s < s1; s++)
+        if (len[s]) f.bytes(ptr[s], len[s]);
+    return f.final();
+}
+
+bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, uint32_t a1, uint32_t b0,
+                  uint32_t b1) {
+    uint32_t sa = a0, sb = b0;
+    uint64_t pa = 0, pb = 0;  // positions inside the current slices
+    for (;;) {
+        while (sa < a1 && pa == len[sa]) { sa++; pa = 0; }
+        while (sb < b1 && pb == len[sb]) { sb++; pb = 0; }
+        const bool ea = sa == a1, eb = sb == b1;
+        if (ea || eb) return ea && eb;
+        const uint64_t k = std::min(len[sa] - pa, len[sb] - pb);
+        if (ptr[sa] + pa != ptr[sb] + pb && memcmp(ptr[sa] + pa, ptr[sb] + pb, k) != 0) return false;
+        pa += k;
+        pb += k;
+    }
+}
+
+uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                    const uint64_t* req_len, uint32_t* rep) {
+    if (n == 0) return 0;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += req_len[i];
+    const int threads = threads_for(total, n);
+    std::vector<uint64_t> fp(n);
+    parallel_for(n, threads, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; i++) fp[i] = fingerprint(ptr, len, first[i], first[i + 1]);
+    });
+    // Tentative representative: first request with the same (fingerprint, length).
+    std::unordered_map<uint64_t, uint32_t> head;
+    head.reserve((size_t)n * 2);
+    std::vector<uint32_t> tent(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t key = fp[i] ^ (req_len[i] * 0x9E3779B97F4A7C15ull);
+        auto it = head.emplace(key, i).first;
+        tent[i] = it->second;
+    }
+    // Confirm byte for byte (in parallel); a mismatch is a fingerprint collision.
+    std::vector<uint8_t> ok(n, 1);
+    parallel_for(n, threads, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; i++) {
+            const uint32_t j = tent[i];
+            if (j != i)
+                ok[i] = req_len[i] == req_len[j] &&
+                        equal_concat(ptr, len, first[i], first[i + 1], first[j], first[j + 1]);
+        }
+    });
+    // Sequential resolution: confirmed -> tentative rep; collided -> search the
+    // distinct representatives already seen under this key (rare).
+    std::unordered_map<uint64_t, std::vector<uint32_t>> reps;  // only keys that collided
+    uint32_t distinct = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t j = tent[i];
+        if (j == i) {
+            rep[i] = i;
+            distinct++;
+            continue;
+        }
+        if (ok[i]) {
+            rep[i] = j;
+            continue;
+        }
+        const uint64_t key = fp[i] ^ (req_len[i] * 0x9E3779B97F4A7C15ull);
+        auto& cand = reps[key];
+        uint32_t found = UINT32_MAX;
+        for (uint32_t r : cand)
+            if (req_len[r] == req_len[i] && equal_concat(ptr, len, first[i], first[i + 1], first[r], first[r + 1])) {
+                found = r;
+                break;
+            }
+        if (found == UINT32_MAX) {
+            cand.push_back(i);
+            rep[i] = i;
+            distinct++;
+        } else {
+            rep[i] = found;
+        }
+    }
+    // rep[i] is the smallest equal index: equal requests share the key, so a
+    // request equal to tent[i] (the key's first index) has rep tent[i]; the
+    // first member of any other class under the key entered `reps` above.
+    return distinct;
+}
+
+void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,
+          uint32_t m, const uint64_t* dst_off, uint8_t* dst, int threads) {
+    parallel_for(m, threads, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t k = lo; k < hi; k++) {
+            const uint32_t i = which ? which[k] : k;
+            uint8_t* d = dst + dst_off[k];
+            for (uint32_t s = first[i]; s < first[i + 1]; s++) {
+                if (len[s]) memcpy(d, ptr[s], len[s]);
+                d += len[s];
+            }
+        }
+    });
+}
+
+}  // namespace host
+}  // namespace mirsha
+
+extern "C" int mirsha_dedup_plan(const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                                 const uint32_t* slice_first, uint32_t n, uint32_t* rep_out,
+                                 uint32_t* n_unique_out) {
+    if (n == 0) {
+        if (n_unique_out) *n_unique_out = 0;
+        return MIRSHA_OK;
+    }
+    if (!slice_first || !rep_out || slice_first[0] != 0) return MIRSHA_EINVAL;
+    const uint32_t ns = slice_first[n];
+    if (ns && (!slice_ptr || !slice_len)) return MIRSHA_EINVAL;
+    std::vector<uint64_t> req_len(n);
+    for (uint32_t i = 0; i < n; i++) {
+        if (slice_first[i + 1] < slice_first[i]) return MIRSHA_EINVAL;
+        uint64_t L = 0;
+        for (uint32_t s = slice_first[i]; s < slice_first[i + 1]; s++) {
+            if (slice_len[s] && !slice_ptr[s]) return MIRSHA_EINVAL;
+            L += slice_len[s];
+        }
+        req_len[i] = L;
+    }
+    const uint32_t u = mirsha::host::dedup_plan(slice_ptr, slice_len, slice_first, n, req_len.data(), rep_out);
+    if (n_unique_out) *n_unique_out = u;
+    return MIRSHA_OK;
+}

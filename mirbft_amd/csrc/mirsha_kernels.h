@@ -10,8 +10,19 @@ constexpr uint32_t kBlockThreads = 64 * kWavesPerBlock;
 constexpr uint32_t kNullIndex = 0xFFFFFFFFu;
 
 // sha256_msgs_kernel variants: loader (LDS-staged / direct per-lane loads) x
-// rounds (generated asm / compiler-scheduled C++).  Default: kVariantLds.
-enum : int { kVariantLds = 0, kVariantDirect = 1, kVariantLdsCxx = 2, kVariantDirectCxx = 3 };
+// rounds (generated asm / compiler-scheduled C++).  Default: kVariantLds, whose
+// launches of at most kLowOccTiles tiles (<= 1 wave per SIMD) take the
+// low-occupancy kernel (prefetching direct loads, no-yield rounds).
+// kVariantLowOcc / kVariantLdsOnly force one of the two at any size (A/B, tests).
+enum : int {
+    kVariantLds = 0,
+    kVariantDirect = 1,
+    kVariantLdsCxx = 2,
+    kVariantDirectCxx = 3,
+    kVariantLowOcc = 4,
+    kVariantLdsOnly = 5
+};
+constexpr uint32_t kLowOccTiles = 1024;  // 256 CUs x 4 SIMDs
 
 // Arenas up to kMaxBufferArena bytes use one 32-bit buffer descriptor; larger
 // ones (any size) the 64-bit per-lane addressed loader.

@@ -17,6 +17,7 @@
 // XOR-swizzled so both the ds_write_b128 (8-lane groups, 128 contiguous bytes)
 // and the per-lane ds_read_b128 (16-lane groups) are bank-conflict free.
 #include <algorithm>
+#include <cstdlib>
 
 #include "mirsha_kernels.h"
 #include "sha256_device.h"
@@ -263,6 +264,53 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     hash_tile<kLds, kAsm, false, kWide>(arena, arena_len, off, len, order, n, out,
                                  __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000), tile[wv], t,
                                  lane);
+}
+
+// Low-occupancy form of the request kernel, for launches of at most one wave
+// per SIMD (a few long messages: e.g. the distinct EpochChange payloads of a
+// deduplicated cycle).  A lone wave's memory latency is not hidden by other
+// waves, so each lane prefetches block b+1's chunks (direct per-lane loads)
+// before compressing block b, and the rounds are the no-yield form (there is
+// no other wave to yield the issue slot to).
+__global__ __launch_bounds__(kBlockThreads) void sha256_msgs_lowocc_kernel(
+    const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t t = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
+    const uint32_t slot = t * 64u + lane;
+    const bool valid = slot < n;
+    const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
+    const uint32_t L = valid ? len[msg] : 0u;
+    const uint32_t o = valid ? (uint32_t)off[msg] : 0u;
+    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
+    const uint32_t wave_nb = wave_max(nb);
+    const uint32_t records = (uint32_t)((arena_len + 3u) & ~3ull);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)records, 0x00020000);
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    RawChunk cur[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, 0u, (uint32_t)q, 0u < nb, cur[q]);
+    for (uint32_t blk = 0; blk < wave_nb; blk++) {
+        // Next block's chunks first; past a lane's last block they are
+        // inactive (range-checked zero reads, no memory access).
+        RawChunk nxt[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, blk + 1u, (uint32_t)q, blk + 1u < nb, nxt[q]);
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            finish_chunk(cur[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
+        // (the latency-ordered rounds_asm_ilp measured no faster here:
+        // 3.03 ms per config-4 launch either way)
+        if (blk < nb) compress_asm_lat(st, w);
+#pragma unroll
+        for (int q = 0; q < 4; q++) cur[q] = nxt[q];
+    }
+    if (valid) store_digest(out, msg, st);
 }
 
 // Dependent pass: message k = concat(digests[idx[e]] for e in [first[k], first[k+1]))
@@ -787,8 +835,13 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_kernel<true, true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
+    if (variant == kVariantLowOcc || (variant == kVariantLds && tiles <= kLowOccTiles)) {
+        sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        return hipGetLastError();
+    }
     switch (variant) {
         case kVariantLds:
+        case kVariantLdsOnly:
             sha256_msgs_kernel<true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
             break;
         case kVariantDirect:

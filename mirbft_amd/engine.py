@@ -32,6 +32,8 @@ VARIANT_LDS = 0
 VARIANT_DIRECT = 1
 VARIANT_LDS_CXX = 2
 VARIANT_DIRECT_CXX = 3
+VARIANT_LOWOCC = 4
+VARIANT_LDS_ONLY = 5
 
 
 def _ptr(a: np.ndarray | None) -> int | None:
@@ -44,6 +46,66 @@ def _as_u8(buf) -> np.ndarray:
     if isinstance(buf, np.ndarray):
         return np.ascontiguousarray(buf.reshape(-1).view(np.uint8))
     return np.frombuffer(memoryview(buf), dtype=np.uint8)
+
+
+class SliceArrays:
+    """HashRequest.Data of n requests as the C-ABI's slice arrays: slice s is
+    ``len[s]`` bytes at address ``ptr[s]``; request i = slices [first[i], first[i+1]).
+    Holds references to the Python buffers the pointers come from."""
+
+    def __init__(self, ptr: np.ndarray, length: np.ndarray, first: np.ndarray, keep=()):
+        self.ptr = np.ascontiguousarray(ptr, dtype=np.uint64)
+        self.len = np.ascontiguousarray(length, dtype=np.uint64)
+        self.first = np.ascontiguousarray(first, dtype=np.uint32)
+        if self.ptr.shape != self.len.shape or self.first.size < 1 or int(self.first[-1]) != self.ptr.size:
+            raise ValueError("inconsistent slice arrays")
+        self.keep = keep
+        self.n = int(self.first.size) - 1
+        self.ptr_p = _ptr(self.ptr)
+        self.len_p = _ptr(self.len)
+        self.first_p = _ptr(self.first)
+
+    @classmethod
+    def from_requests(cls, requests: Sequence[Sequence[bytes]]) -> "SliceArrays":
+        keep, lens, first = [], [], [0]
+        for req in requests:
+            for s in req:
+                b = bytes(s)
+                keep.append(b)
+                lens.append(len(b))
+            first.append(len(keep))
+        ptr = np.zeros(len(keep), dtype=np.uint64)
+        for i, b in enumerate(keep):
+            if len(b):
+                ptr[i] = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value
+        return cls(ptr, np.asarray(lens, dtype=np.uint64), np.asarray(first, dtype=np.uint32), keep)
+
+    @classmethod
+    def from_buffer(cls, buf: np.ndarray, slice_off: np.ndarray, slice_len: np.ndarray, first: np.ndarray):
+        """Slices that are byte ranges of one numpy buffer (vectorised; for large streams)."""
+        b = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+        base = b.ctypes.data
+        off = np.ascontiguousarray(slice_off, dtype=np.uint64)
+        return cls(np.uint64(base) + off, slice_len, first, (b,))
+
+
+class Ticket:
+    """A submission of Engine.submit_slices; ``out`` receives the digests."""
+
+    def __init__(self, value: int, out: np.ndarray):
+        self.value = value
+        self.out = out
+
+
+def dedup_plan(requests) -> tuple[np.ndarray, int]:
+    """Host-only dedup plan (mirsha_dedup_plan): rep[i] = smallest j <= i with
+    identical request bytes; returns (rep, number of distinct requests)."""
+    sl = requests if isinstance(requests, SliceArrays) else SliceArrays.from_requests(requests)
+    rep = np.empty(sl.n, dtype=np.uint32)
+    u = ctypes.c_uint32(0)
+    rc = _lib.load().mirsha_dedup_plan(sl.ptr_p, sl.len_p, sl.first_p, sl.n, _ptr(rep), ctypes.byref(u))
+    check(rc)
+    return rep, u.value
 
 
 def device_count() -> int:
@@ -63,6 +125,7 @@ class Engine:
             raise MirshaError(rc, f"cannot create a gfx950 context on device {device}")
         self.ctx = ctx
         self.device = device
+        self.last_unique = 0
 
     # ------------------------------------------------------------ lifecycle
     def close(self) -> None:
@@ -134,30 +197,50 @@ class Engine:
         arena = b"".join(messages)
         return self.hash_batch(arena, off, lens)
 
-    def hash_slices(self, requests: Sequence[Sequence[bytes]]) -> np.ndarray:
-        """Digest of concat(req) for each req = HashRequest.Data (actions.go:157-164)."""
-        n = len(requests)
+    def hash_slices(self, requests: Sequence[Sequence[bytes]], dedup: bool = False) -> np.ndarray:
+        """Digest of concat(req) for each req = HashRequest.Data (actions.go:157-164).
+        dedup=True hashes each distinct content once (mirsha_hash_slices_dedup);
+        ``self.last_unique`` then holds the number of distinct requests."""
+        sl = SliceArrays.from_requests(requests)
+        return self.hash_slice_arrays(sl, dedup)
+
+    def hash_slice_arrays(self, sl: "SliceArrays", dedup: bool = False) -> np.ndarray:
+        """hash_slices over prepared slice arrays (pointer / length / first)."""
+        n = sl.n
         out = np.empty((n, 32), dtype=np.uint8)
         if n == 0:
+            self.last_unique = 0
             return out
-        keep = []
-        ptrs, lens, first = [], [], [0]
-        for req in requests:
-            for s in req:
-                b = bytes(s)
-                keep.append(b)
-                lens.append(len(b))
-            first.append(len(keep))
-        ns = len(keep)
-        ptr_arr = (ctypes.c_void_p * max(ns, 1))()
-        for i, b in enumerate(keep):
-            ptr_arr[i] = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value if len(b) else None
-        len_arr = np.asarray(lens if ns else [0], dtype=np.uint64)
-        first_arr = np.asarray(first, dtype=np.uint32)
-        self._check(
-            self._lib.mirsha_hash_slices(self.ctx, ctypes.addressof(ptr_arr), _ptr(len_arr), _ptr(first_arr), n, _ptr(out))
-        )
+        if dedup:
+            u = ctypes.c_uint32(0)
+            self._check(self._lib.mirsha_hash_slices_dedup(self.ctx, sl.ptr_p, sl.len_p, sl.first_p, n, _ptr(out),
+                                                           ctypes.byref(u)))
+            self.last_unique = u.value
+        else:
+            self._check(self._lib.mirsha_hash_slices(self.ctx, sl.ptr_p, sl.len_p, sl.first_p, n, _ptr(out)))
+            self.last_unique = n
         return out
+
+    def submit_slices(self, requests, dedup: bool = False) -> "Ticket":
+        """Asynchronous, order-preserving submission (mirsha_submit_slices): the
+        requests are packed before this returns; ``wait(ticket)`` yields the
+        digests in origin order.  ``requests`` may be a list of slice lists or
+        a SliceArrays."""
+        sl = requests if isinstance(requests, SliceArrays) else SliceArrays.from_requests(requests)
+        out = np.empty((sl.n, 32), dtype=np.uint8)
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.mirsha_submit_slices(self.ctx, sl.ptr_p, sl.len_p, sl.first_p, sl.n, _ptr(out),
+                                                   _lib.MIRSHA_SUBMIT_DEDUP if dedup else 0, ctypes.byref(t)))
+        return Ticket(t.value, out)
+
+    def wait(self, ticket: "Ticket") -> np.ndarray:
+        self._check(self._lib.mirsha_wait(self.ctx, ticket.value))
+        return ticket.out
+
+    def poll(self, ticket: "Ticket") -> bool:
+        done = ctypes.c_int(0)
+        self._check(self._lib.mirsha_poll(self.ctx, ticket.value, ctypes.byref(done)))
+        return bool(done.value)
 
     def hash_requests_then_batches(self, arena, off, length, idx, batch_first):
         """Request digests, then batch digests over them on device (sequence.go:154-157)."""
@@ -314,6 +397,9 @@ def hash_batch_multi(devices: Iterable[int], arena, off, length) -> np.ndarray:
 
 __all__ = [
     "Engine",
+    "SliceArrays",
+    "Ticket",
+    "dedup_plan",
     "Pipeline",
     "bucket_order",
     "device_count",
@@ -330,4 +416,6 @@ __all__ = [
     "PIPELINE_AUTO",
     "VARIANT_LDS",
     "VARIANT_DIRECT",
+    "VARIANT_LOWOCC",
+    "VARIANT_LDS_ONLY",
 ]

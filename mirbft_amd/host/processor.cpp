@@ -1,6 +1,7 @@
 // processor.cpp — see processor.hpp.
 #include "processor.hpp"
 
+#include <algorithm>
 #include <cstring>
 
 #include "../../include/mirsha.h"
@@ -22,23 +23,52 @@ GpuEngine::GpuEngine(int device) {
 
 GpuEngine::~GpuEngine() { mirsha_ctx_destroy(ctx_); }
 
-void GpuEngine::HashBatch(const std::vector<const HashRequest*>& reqs,
-                          std::vector<std::array<uint8_t, 32>>& out) {
-    const uint32_t n = (uint32_t)reqs.size();
-    out.resize(n);
-    if (n == 0) return;
+namespace {
+struct SliceLists {
     std::vector<const uint8_t*> ptr;
     std::vector<uint64_t> len;
-    std::vector<uint32_t> first(n + 1, 0);
-    for (uint32_t i = 0; i < n; i++) {
-        for (const Bytes& b : reqs[i]->Data) {  // for _, data := range req.Data (processor.go:135)
-            ptr.push_back(b.data);
-            len.push_back(b.size);
+    std::vector<uint32_t> first;
+    explicit SliceLists(const std::vector<const HashRequest*>& reqs) : first(reqs.size() + 1, 0) {
+        for (size_t i = 0; i < reqs.size(); i++) {
+            for (const Bytes& b : reqs[i]->Data) {  // for _, data := range req.Data (processor.go:135)
+                ptr.push_back(b.data);
+                len.push_back(b.size);
+            }
+            first[i + 1] = (uint32_t)ptr.size();
         }
-        first[i + 1] = (uint32_t)ptr.size();
     }
-    int rc = mirsha_hash_slices(ctx_, ptr.data(), len.data(), first.data(), n, out[0].data());
+};
+}  // namespace
+
+void GpuEngine::HashBatch(const std::vector<const HashRequest*>& reqs, std::vector<std::array<uint8_t, 32>>& out,
+                          bool dedup, uint32_t* unique) {
+    const uint32_t n = (uint32_t)reqs.size();
+    out.resize(n);
+    if (unique) *unique = n;
+    if (n == 0) return;
+    SliceLists sl(reqs);
+    int rc = dedup ? mirsha_hash_slices_dedup(ctx_, sl.ptr.data(), sl.len.data(), sl.first.data(), n, out[0].data(),
+                                              unique)
+                   : mirsha_hash_slices(ctx_, sl.ptr.data(), sl.len.data(), sl.first.data(), n, out[0].data());
     if (rc != MIRSHA_OK) panic(ctx_, rc, "could not hash requests");
+}
+
+uint64_t GpuEngine::Submit(const std::vector<const HashRequest*>& reqs, std::vector<std::array<uint8_t, 32>>& out,
+                           bool dedup) {
+    const uint32_t n = (uint32_t)reqs.size();
+    out.resize(std::max<uint32_t>(n, 1));
+    SliceLists sl(reqs);
+    uint64_t ticket = 0;
+    int rc = mirsha_submit_slices(ctx_, sl.ptr.data(), sl.len.data(), sl.first.data(), n, out[0].data(),
+                                  dedup ? MIRSHA_SUBMIT_DEDUP : 0, &ticket);
+    if (rc != MIRSHA_OK) panic(ctx_, rc, "could not submit requests");
+    out.resize(n);  // no reallocation: n <= capacity
+    return ticket;
+}
+
+void GpuEngine::Wait(uint64_t ticket) {
+    int rc = mirsha_wait(ctx_, ticket);
+    if (rc != MIRSHA_OK) panic(ctx_, rc, "could not collect digests");
 }
 
 namespace {
@@ -63,32 +93,73 @@ private:
 
 std::unique_ptr<Hash> NewGpuSha256(GpuEngine& engine) { return std::make_unique<GpuSha256>(engine); }
 
-ActionResults Processor::Process(const Actions& actions) {
+namespace {
+ActionResults make_results(const std::vector<const HashRequest*>& reqs,
+                           const std::vector<std::array<uint8_t, 32>>& digests) {
     ActionResults results;
-    std::vector<std::array<uint8_t, 32>> digests;
-    engine_.HashBatch(actions.Hash, digests);  // one device call per Ready() cycle
-    results.Digests.resize(actions.Hash.size());
-    for (size_t i = 0; i < actions.Hash.size(); i++) {  // Digests[i] for actions.Hash[i] (processor.go:139)
-        results.Digests[i].Request = actions.Hash[i];
+    results.Digests.resize(reqs.size());
+    for (size_t i = 0; i < reqs.size(); i++) {  // Digests[i] for actions.Hash[i] (processor.go:139)
+        results.Digests[i].Request = reqs[i];
         results.Digests[i].Digest = digests[i];
     }
     return results;
+}
+}  // namespace
+
+ActionResults Processor::Process(const Actions& actions) {
+    std::vector<std::array<uint8_t, 32>> digests;
+    engine_.HashBatch(actions.Hash, digests, dedup_);  // one device call per Ready() cycle
+    return make_results(actions.Hash, digests);
+}
+
+PendingResults Processor::Submit(const Actions& actions) {
+    PendingResults p;
+    p.engine_ = &engine_;
+    p.reqs_ = actions.Hash;
+    p.digests_ = std::make_unique<std::vector<std::array<uint8_t, 32>>>();
+    if (!p.reqs_.empty()) p.ticket_ = engine_.Submit(p.reqs_, *p.digests_, dedup_);
+    return p;
+}
+
+ActionResults PendingResults::Wait() {
+    if (ticket_) {
+        engine_->Wait(ticket_);
+        ticket_ = 0;
+    }
+    return make_results(reqs_, *digests_);
 }
 
 }  // namespace mirbft
 
 extern "C" int mirbft_host_process(int device, const uint8_t* const* data, const uint64_t* len, uint32_t n,
                                    uint8_t* digests_out, char* err, uint32_t err_len) {
+    return mirbft_host_process_ex(device, data, len, n, digests_out, 0, nullptr, err, err_len);
+}
+
+extern "C" int mirbft_host_process_ex(int device, const uint8_t* const* data, const uint64_t* len, uint32_t n,
+                                      uint8_t* digests_out, int flags, uint32_t* unique_out, char* err,
+                                      uint32_t err_len) {
     try {
         mirbft::GpuEngine engine(device);
-        mirbft::Processor p(engine);
+        mirbft::Processor p(engine, (flags & 1) != 0);
         std::vector<mirbft::HashRequest> reqs(n);
         mirbft::Actions a;
         for (uint32_t i = 0; i < n; i++) {
             reqs[i].Data.push_back(mirbft::Bytes{data[i], (size_t)len[i]});
             a.Hash.push_back(&reqs[i]);
         }
-        mirbft::ActionResults r = p.Process(a);
+        mirbft::ActionResults r;
+        if (flags & 2) {
+            mirbft::PendingResults pending = p.Submit(a);
+            r = pending.Wait();
+        } else {
+            r = p.Process(a);
+        }
+        if (unique_out) {
+            std::vector<std::array<uint8_t, 32>> tmp;
+            *unique_out = n;
+            if (flags & 1) engine.HashBatch(a.Hash, tmp, true, unique_out);
+        }
         for (uint32_t i = 0; i < n; i++) {
             if (r.Digests[i].Request != &reqs[i]) throw std::runtime_error("origin order violated");
             memcpy(digests_out + 32ull * i, r.Digests[i].Digest.data(), 32);

@@ -13,6 +13,10 @@
 // batched device call (mirsha_hash_slices) and returns Digests[i] for
 // actions.Hash[i] with the Request back-pointer, in origin order.  Failures
 // throw std::runtime_error — the reference panics (processor.go:75,81,85,91).
+// Options: dedup (hash each distinct request content once per cycle,
+// mirsha_hash_slices_dedup) and the asynchronous Submit / Pending::Wait form
+// (mirsha_submit_slices / mirsha_wait) for overlapping the cycle's hashing
+// with its WAL writes and sends, as ProcessorWorkPool does (processor.go:447-470).
 #pragma once
 #include <array>
 #include <cstdint>
@@ -69,7 +73,14 @@ public:
     GpuEngine& operator=(const GpuEngine&) = delete;
 
     // Digests of reqs[i] (concat of its Data slices) at out[i], origin order.
-    void HashBatch(const std::vector<const HashRequest*>& reqs, std::vector<std::array<uint8_t, 32>>& out);
+    // dedup: identical requests are hashed once; *unique = distinct requests.
+    void HashBatch(const std::vector<const HashRequest*>& reqs, std::vector<std::array<uint8_t, 32>>& out,
+                   bool dedup = false, uint32_t* unique = nullptr);
+    // Asynchronous form: packs reqs before returning; `out` (resized here) is
+    // filled, in origin order, by Wait(ticket).
+    uint64_t Submit(const std::vector<const HashRequest*>& reqs, std::vector<std::array<uint8_t, 32>>& out,
+                    bool dedup = false);
+    void Wait(uint64_t ticket);
     mirsha_ctx* ctx() { return ctx_; }
 
 private:
@@ -79,14 +90,30 @@ private:
 // hash.Hash whose Sum runs on the GPU (buffers its writes).
 std::unique_ptr<Hash> NewGpuSha256(GpuEngine& engine);
 
+// One submitted cycle; Wait() returns its ActionResults (origin order).
+class PendingResults {
+public:
+    ActionResults Wait();
+
+private:
+    friend class Processor;
+    GpuEngine* engine_ = nullptr;
+    uint64_t ticket_ = 0;
+    std::vector<const HashRequest*> reqs_;
+    std::unique_ptr<std::vector<std::array<uint8_t, 32>>> digests_;
+};
+
 class Processor {
 public:
-    explicit Processor(GpuEngine& engine) : engine_(engine) {}
+    explicit Processor(GpuEngine& engine, bool dedup = false) : engine_(engine), dedup_(dedup) {}
     // processor.go:129-143, batched.
     ActionResults Process(const Actions& actions);
+    // Asynchronous Process: queue the cycle's hashing and return at once.
+    PendingResults Submit(const Actions& actions);
 
 private:
     GpuEngine& engine_;
+    bool dedup_;
 };
 
 }  // namespace mirbft
@@ -96,4 +123,7 @@ extern "C" {
 // mirbft::Processor (exercises the C++ mirror end to end).
 int mirbft_host_process(int device, const uint8_t* const* data, const uint64_t* len, uint32_t n,
                         uint8_t* digests_out, char* err, uint32_t err_len);
+// flags: bit 0 = dedup, bit 1 = asynchronous (Submit, then Wait).
+int mirbft_host_process_ex(int device, const uint8_t* const* data, const uint64_t* len, uint32_t n,
+                           uint8_t* digests_out, int flags, uint32_t* unique_out, char* err, uint32_t err_len);
 }

@@ -15,6 +15,13 @@ with the request back-pointer (origin order).  The reference's work pool
 returns digests in completion order (processor.go:349-356); this one keeps
 origin order, which is a legal (and deterministic) completion order.
 Failures raise (the reference panics, processor.go:75,81,85,91).
+
+``dedup=True`` hashes each distinct request content once per cycle and hands
+every duplicate its own digest (epoch-change acks: applyEpochChangeAckMsg,
+epoch_target.go:459-477).  ``Processor.submit`` / ``PendingResults.wait`` is
+the asynchronous form (mirsha_submit_slices / mirsha_wait): the cycle's
+requests are packed before ``submit`` returns and the digests are collected,
+in origin order, after the caller's other work for the cycle.
 """
 from __future__ import annotations
 
@@ -76,21 +83,48 @@ def gpu_hasher(engine: Engine) -> Callable[[], GpuHash]:
     return lambda: GpuHash(engine)
 
 
+def _results(reqs, digests) -> ActionResults:
+    results = ActionResults(digests=[None] * len(reqs))
+    for i, req in enumerate(reqs):  # Digests[i] for actions.Hash[i] (processor.go:139)
+        results.digests[i] = HashResult(digest=digests[i].tobytes(), request=req)
+    return results
+
+
+class PendingResults:
+    """Hash results of one submitted cycle; ``wait()`` returns its ActionResults."""
+
+    def __init__(self, engine: Engine, reqs, ticket):
+        self._engine, self._reqs, self._ticket = engine, reqs, ticket
+        self._results: Optional[ActionResults] = None
+
+    def done(self) -> bool:
+        return self._results is not None or self._ticket is None or self._engine.poll(self._ticket)
+
+    def wait(self) -> ActionResults:
+        if self._results is None:
+            digests = self._engine.wait(self._ticket) if self._ticket is not None else []
+            self._results = _results(self._reqs, digests)
+        return self._results
+
+
 class Processor:
     """Hash stage of mirbft.Processor; batches one Ready() cycle per device call."""
 
-    def __init__(self, engine: Optional[Engine] = None, device: int = 0):
+    def __init__(self, engine: Optional[Engine] = None, device: int = 0, dedup: bool = False):
         self.engine = engine if engine is not None else Engine(device)
+        self.dedup = dedup
 
     def process(self, actions: Actions) -> ActionResults:
         reqs = actions.hash
-        results = ActionResults(digests=[None] * len(reqs))
         if not reqs:
-            return results
-        digests = self.engine.hash_slices([r.data for r in reqs])
-        for i, req in enumerate(reqs):  # Digests[i] for actions.Hash[i] (processor.go:139)
-            results.digests[i] = HashResult(digest=digests[i].tobytes(), request=req)
-        return results
+            return ActionResults(digests=[])
+        return _results(reqs, self.engine.hash_slices([r.data for r in reqs], dedup=self.dedup))
+
+    def submit(self, actions: Actions) -> PendingResults:
+        """Asynchronous process(): queue the cycle's hashing, return at once."""
+        reqs = list(actions.hash)
+        ticket = self.engine.submit_slices([r.data for r in reqs], dedup=self.dedup) if reqs else None
+        return PendingResults(self.engine, reqs, ticket)
 
 
 class ProcessorWorkPool(Processor):
@@ -101,14 +135,21 @@ class ProcessorWorkPool(Processor):
     """
 
     def __init__(self, engine: Optional[Engine] = None, device: int = 0, hash_workers: int = 0,
-                 transmit_workers: int = 0):
-        super().__init__(engine, device)
+                 transmit_workers: int = 0, dedup: bool = False):
+        super().__init__(engine, device, dedup)
         self._mutex = threading.Lock()
         self.hash_workers = hash_workers
 
-    def process(self, actions: Actions) -> ActionResults:
+    def process(self, actions: Actions, overlap: Optional[Callable[[], Any]] = None) -> ActionResults:
+        """processor.go:447-470: the pool hashes while the WAL and the sends
+        proceed.  Here the cycle's hashing is submitted first, ``overlap()``
+        (the caller's persist / transmit work) runs while the GPU hashes, then
+        the digests are collected in origin order."""
         with self._mutex:  # processor.go:448-449
-            return super().process(actions)
+            pending = self.submit(actions)
+            if overlap is not None:
+                overlap()
+            return pending.wait()
 
     def stop(self) -> None:
         pass

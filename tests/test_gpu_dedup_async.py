@@ -1,0 +1,149 @@
+"""GPU parity of the dedup and asynchronous, order-preserving
+(§8 f3) entry points, through the C-ABI: bit-exact against hashlib (the
+FIPS 180-4 oracle, pinned in test_oracle_golden.py) in origin order."""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+
+from mirbft_amd import (Actions, HashRequest, Processor, ProcessorWorkPool, SliceArrays, hashdata)
+from mirbft_amd import _lib
+from test_host_dedup import python_plan, random_requests
+
+pytestmark = pytest.mark.gpu
+
+
+def want(requests):
+    return [hashlib.sha256(b"".join(bytes(s) for s in r)).digest() for r in requests]
+
+
+def rows(a):
+    return [r.tobytes() for r in a]
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_dedup_random(engine, seed):
+    reqs = random_requests(seed, n=500)
+    got = engine.hash_slices(reqs, dedup=True)
+    assert rows(got) == want(reqs)
+    assert engine.last_unique == python_plan(reqs)[1]
+
+
+def test_dedup_epoch_change_cycle(engine):
+    n_nodes, n_req = 16, 256  # every origin relayed by 16 sources
+    buf, so, sl, first, origin = hashdata.epoch_change_cycle(n_nodes, n_req, 3, 120, 120)
+    arrays = SliceArrays.from_buffer(buf, so, sl, first)
+    got = engine.hash_slice_arrays(arrays, dedup=True)
+    assert engine.last_unique == n_nodes
+    payload = [hashlib.sha256(hashdata.concat(hashdata.epoch_change_payload(2, o, 3, 120, 120))).digest()
+               for o in range(n_nodes)]
+    assert rows(got) == [payload[o] for o in origin]
+    plain = engine.hash_slice_arrays(arrays, dedup=False)
+    assert np.array_equal(plain, got)
+
+
+def test_dedup_all_distinct_and_all_equal(engine):
+    distinct = [[bytes([i]) * (i + 1)] for i in range(100)]
+    assert rows(engine.hash_slices(distinct, dedup=True)) == want(distinct)
+    assert engine.last_unique == 100
+    same = [[b"x" * 5000]] * 77 + [[b"x" * 2500, b"x" * 2500]]
+    assert rows(engine.hash_slices(same, dedup=True)) == want(same)
+    assert engine.last_unique == 1
+    empties = [[], [b""], [b"", b""]]
+    assert rows(engine.hash_slices(empties, dedup=True)) == want(empties)
+    assert engine.last_unique == 1
+    assert engine.hash_slices([], dedup=True).shape == (0, 32)
+
+
+def test_async_order_and_ring_retirement(engine):
+    """Nine submissions (more than the 4-slot ring) of different shapes, some
+    deduplicated; waits out of order; every ticket's digests in origin order."""
+    batches = [random_requests(s, n=50 + 40 * s) for s in range(9)]
+    tickets = [engine.submit_slices(b, dedup=bool(s % 2)) for s, b in enumerate(batches)]
+    assert [t.value for t in tickets] == sorted(t.value for t in tickets)
+    # waiting for a later ticket completes every earlier one too
+    assert rows(engine.wait(tickets[5])) == want(batches[5])
+    for s in (0, 3, 1, 2, 4):
+        assert engine.poll(tickets[s])
+        assert rows(tickets[s].out) == want(batches[s])
+    for s in (8, 6, 7):
+        assert rows(engine.wait(tickets[s])) == want(batches[s])
+
+
+def test_async_poll_and_empty_submission(engine):
+    t0 = engine.submit_slices([])
+    assert engine.wait(t0).shape == (0, 32)
+    reqs = [[b"abc"] * k for k in range(1, 200)]
+    t = engine.submit_slices(reqs)
+    while not engine.poll(t):
+        pass
+    assert rows(t.out) == want(reqs)
+
+
+def test_async_caller_may_reuse_slices_after_submit(engine):
+    buf = bytearray(b"q" * 4096)
+    arr = np.frombuffer(buf, dtype=np.uint8)
+    sl = SliceArrays.from_buffer(arr, np.arange(64, dtype=np.uint64) * 64, np.full(64, 64, dtype=np.uint64),
+                                 np.arange(65, dtype=np.uint32))
+    t = engine.submit_slices(sl)
+    expect = [hashlib.sha256(bytes(buf[64 * i: 64 * i + 64])).digest() for i in range(64)]
+    arr[:] = 0  # the library packed the bytes before submit returned
+    assert rows(engine.wait(t)) == expect
+
+
+def test_invalid_ticket_raises(engine):
+    from mirbft_amd import MirshaError
+    from mirbft_amd.engine import Ticket
+
+    with pytest.raises(MirshaError):
+        engine.wait(Ticket(10 ** 9, np.empty((0, 32), np.uint8)))
+    sl = SliceArrays.from_requests([[b"a"]])
+    out = np.empty((1, 32), np.uint8)
+    t = ctypes.c_uint64(0)
+    with pytest.raises(MirshaError):  # unknown flag bit
+        engine._check(engine._lib.mirsha_submit_slices(engine.ctx, sl.ptr_p, sl.len_p, sl.first_p, 1,
+                                                       out.ctypes.data, 0x80, ctypes.byref(t)))
+
+
+def test_processor_dedup_and_submit(engine):
+    reqs = [HashRequest(data=d, origin=i) for i, d in enumerate(random_requests(7, n=120))]
+    p = Processor(engine, dedup=True)
+    r = p.process(Actions(hash=reqs))
+    assert [x.request for x in r.digests] == reqs
+    assert [x.digest for x in r.digests] == want([q.data for q in reqs])
+    pending = Processor(engine).submit(Actions(hash=reqs))
+    r2 = pending.wait()
+    assert [x.request for x in r2.digests] == reqs
+    assert [x.digest for x in r2.digests] == want([q.data for q in reqs])
+    assert pending.done()
+    assert Processor(engine).submit(Actions(hash=[])).wait().digests == []
+
+
+def test_work_pool_overlap(engine):
+    reqs = [HashRequest(data=d) for d in random_requests(8, n=90)]
+    ran = []
+    r = ProcessorWorkPool(engine, dedup=True).process(Actions(hash=reqs), overlap=lambda: ran.append(1))
+    assert ran == [1]
+    assert [x.digest for x in r.digests] == want([q.data for q in reqs])
+    assert [x.request for x in r.digests] == reqs
+
+
+@pytest.mark.parametrize("flags", [1, 2, 3])
+def test_cpp_mirror_dedup_async(flags):
+    host = ctypes.CDLL(_lib.HOST_LIB_PATH)
+    msgs = [b"m" * (i % 7) * 50 for i in range(100)]
+    bufs = [ctypes.create_string_buffer(m, len(m) or 1) for m in msgs]
+    data = (ctypes.c_void_p * len(msgs))(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_uint64 * len(msgs))(*[len(m) for m in msgs])
+    out = (ctypes.c_uint8 * (32 * len(msgs)))()
+    uniq = ctypes.c_uint32(0)
+    err = ctypes.create_string_buffer(256)
+    host.mirbft_host_process_ex.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p,
+                                            ctypes.c_uint32]
+    rc = host.mirbft_host_process_ex(0, data, lens, len(msgs), out, flags, ctypes.byref(uniq), err, 256)
+    assert rc == 0, err.value
+    got = [bytes(out[32 * i: 32 * i + 32]) for i in range(len(msgs))]
+    assert got == [hashlib.sha256(m).digest() for m in msgs]
+    assert uniq.value == (7 if flags & 1 else len(msgs))
