@@ -520,7 +520,7 @@ def main():
                 "workload": f"config{a.config}: {wl.desc}",
                 **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only"][a.variant],
+                "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only", "pair"][a.variant],
             },
             "gb_per_s_hashed": gbps,
             "roofline": {

@@ -73,11 +73,15 @@ void* mirsha_ctx_stream(mirsha_ctx* ctx);
 
 /* Kernel variant for sha256 over packed messages (A/B measurement):
  * 0 = LDS-staged coalesced loader + generated-asm rounds (default; a launch
- *     of at most 1024 waves -- one per SIMD -- takes the low-occupancy kernel:
- *     prefetching direct loads, no-yield rounds),
+ *     of at most 512 64-message groups takes the producer/consumer pair
+ *     kernel -- schedule and rounds of each compression on two waves on two
+ *     SIMDs -- and one of at most 1024 groups (one wave per SIMD) the
+ *     low-occupancy kernel: prefetching direct loads, no-yield rounds;
+ *     MIRSHA_PAIR=0 in the environment disables the pair forms),
  * 1 = direct per-lane loads + asm rounds, 2 = LDS loader + compiler-scheduled
  * C++ rounds, 3 = direct loads + C++ rounds, 4 = the low-occupancy kernel at
- * any size, 5 = the LDS kernel at any size.  All are bit-exact. */
+ * any size, 5 = the LDS kernel at any size, 6 = the pair kernel at any size.
+ * All are bit-exact. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
 /* Per-kernel device-time accounting with HIP events on the launch stream.

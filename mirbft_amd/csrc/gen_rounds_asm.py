@@ -188,6 +188,50 @@ def emit_fn_ilp(name):
     return out
 
 
+def block_kw():
+    """Consumer rounds of the producer/consumer pair kernels: 8 rounds whose
+    K[j] + W[j] arrive precomputed (%14..%21, from the producer wave through
+    LDS), so no message schedule here: 14 instructions per round, ordered
+    for a lone wave (h += KW first, the e- and a-side rotations interleaved)."""
+    T = [op(8 + i) for i in range(6)]
+    lines = []
+    for r in range(8):
+        a, b, c, d, e, f, g, h = [op((k - r) % 8) for k in range(8)]
+        kw = op(14 + r)
+        lines += [
+            f"v_add_u32_e32 {h}, {h}, {kw}",
+            f"v_alignbit_b32 {T[0]}, {e}, {e}, 6",
+            f"v_alignbit_b32 {T[3]}, {a}, {a}, 2",
+            f"v_alignbit_b32 {T[1]}, {e}, {e}, 11",
+            f"v_alignbit_b32 {T[4]}, {a}, {a}, 13",
+            f"v_alignbit_b32 {T[2]}, {e}, {e}, 25",
+            f"v_alignbit_b32 {T[5]}, {a}, {a}, 22",
+            f"v_bitop3_b32 {T[0]}, {T[0]}, {T[1]}, {T[2]} bitop3:0x96",
+            f"v_bitop3_b32 {T[1]}, {e}, {f}, {g} bitop3:0xca",
+            f"v_bitop3_b32 {T[3]}, {T[3]}, {T[4]}, {T[5]} bitop3:0x96",
+            f"v_bitop3_b32 {T[4]}, {a}, {b}, {c} bitop3:0xe8",
+            f"v_add3_u32 {h}, {h}, {T[0]}, {T[1]}",
+            f"v_add_u32_e32 {d}, {d}, {h}",
+            f"v_add3_u32 {h}, {h}, {T[3]}, {T[4]}",
+        ]
+    return lines
+
+
+def emit_fn_kw(name):
+    out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint4 k0, uint4 k1) {{",
+           "    uint32_t t0, t1, t2, t3, t4, t5;",
+           "    asm volatile("]
+    for ln in block_kw():
+        out.append(f'        "{ln}\\n\\t"')
+    outs = ", ".join([f'"+v"(s[{i}])' for i in range(8)] + [f'"=&v"(t{i})' for i in range(6)])
+    ins = ", ".join(f'"v"({v})' for v in ("k0.x", "k0.y", "k0.z", "k0.w", "k1.x", "k1.y", "k1.z", "k1.w"))
+    out.append(f"        : {outs}")
+    out.append(f"        : {ins});")
+    out.append("}")
+    out.append("")
+    return out
+
+
 VARIANTS = {
     # name: (ch_mode, add_mode, k_mode, nops)
     "rounds_asm": ("bitop3", "add3", "sgpr", True),
@@ -238,6 +282,9 @@ def emit():
         out += emit_fn(name, ch, ad, km, nops)
     out.append("// Latency-oriented order (lone waves): same instructions, 12 temporaries.")
     out += emit_fn_ilp("rounds_asm_ilp")
+    out.append("// 8 consumer rounds with K + W precomputed (pair kernels): names rotate")
+    out.append("// back after 8 rounds, so the same statement serves every 8-round chunk.")
+    out += emit_fn_kw("rounds_kw8_asm")
     out.append("}  // namespace mirsha")
     return "\n".join(out) + "\n"
 

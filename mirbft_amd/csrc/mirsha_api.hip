@@ -479,6 +479,11 @@ int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint
                 }))
                 return rc;
         }
+        if (mirsha::pairs_enabled() && (p->n_lists + 63u) / 64u <= mirsha::kPairMaxGroups)
+            return timed_launch(c, 1, [&] {  // few long chains: producer/consumer pairs
+                return mirsha::launch_chain_pair(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
+                                                 p->d_cfirst.as<uint32_t>(), p->n_lists, d_list_out, c->stream);
+            });
         return timed_launch(c, 1, [&] {
             return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
                                         p->d_cfirst.as<uint32_t>(), p->n_lists, 0u, mirsha::kOpenEnd,
@@ -940,7 +945,7 @@ int mirsha_ctx_set_stream(mirsha_ctx* c, void* s) {
 void* mirsha_ctx_stream(mirsha_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
 
 int mirsha_ctx_set_variant(mirsha_ctx* c, int v) {
-    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantLdsOnly) return MIRSHA_EINVAL;
+    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantPair) return MIRSHA_EINVAL;
     c->variant = v;
     return MIRSHA_OK;
 }

@@ -20,9 +20,15 @@ enum : int {
     kVariantLdsCxx = 2,
     kVariantDirectCxx = 3,
     kVariantLowOcc = 4,
-    kVariantLdsOnly = 5
+    kVariantLdsOnly = 5,
+    kVariantPair = 6
 };
-constexpr uint32_t kLowOccTiles = 1024;  // 256 CUs x 4 SIMDs
+constexpr uint32_t kLowOccTiles = 1024;   // 256 CUs x 4 SIMDs
+// Small launches take a latency form: at most kPairMaxGroups 64-message groups
+// the producer/consumer pair kernels (<= 2 pairs per CU: every wave alone on
+// a SIMD).  MIRSHA_PAIR=0 in the environment turns the automatic choice off.
+constexpr uint32_t kPairMaxGroups = 512;
+bool pairs_enabled();
 
 // Arenas up to kMaxBufferArena bytes use one 32-bit buffer descriptor; larger
 // ones (any size) the 64-bit per-lane addressed loader.
@@ -42,6 +48,10 @@ constexpr uint32_t kOpenEnd = 0xFFFFFFFEu;
 hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                         const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
                         uint8_t* out, hipStream_t s);
+// Whole (compacted) list chains by producer/consumer pairs, one 128-thread
+// workgroup per 64 lists; for at most kPairMaxGroups groups.
+hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
+                             const uint32_t* cfirst, uint32_t n_lists, uint8_t* out, hipStream_t s);
 // Fused request -> list pass (one persistent launch), see mirsha_kernels.hip.
 constexpr uint32_t kFusedChunkBlocks = 4;  // list blocks (8 digests) per readiness chunk
 constexpr uint32_t kCtlTileTicket = 0, kCtlListTicket = 16, kCtlError = 32, kCtlWords = 48;  // u64 words

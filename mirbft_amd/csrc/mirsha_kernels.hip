@@ -313,6 +313,203 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_lowocc_kernel(
     if (valid) store_digest(out, msg, st);
 }
 
+// ---- producer / consumer pairs (wavefront-cooperative multi-block hashing) --
+// When there are fewer 64-message groups than SIMDs, every group's wave runs
+// alone on its SIMD and its time is one long dependent chain of compressions
+// (a VerifyBatch of 500 digests is 251 of them), paced by what ONE wave can
+// issue (~4 cycles per instruction).  A pair splits the compression's
+// instruction stream over two waves of one 128-thread workgroup, which the
+// dispatcher always places on two different SIMDs (tools/simd_probe.hip):
+//   wave 0 (producer): loads block b+1, builds its 16 words, computes the
+//     message schedule W[16..63] and K[j] + W[j] (~600 instructions) and
+//     writes the 64 KW words to an LDS ring slot;
+//   wave 1 (consumer): runs the 64 rounds of block b from the other slot
+//     (rounds_kw8_asm: 14 instructions per round, ~900 per block).
+// One workgroup barrier per block hands the slots over.
+constexpr uint32_t kPairThreads = 128;
+
+struct PairRing {
+    uint4 kw[2][16][64];  // [slot][quad of 4 KW words][lane]: 16 B per lane, conflict-free b128 access
+};
+
+// Message schedule + round constants of one block into a ring slot.
+__device__ __forceinline__ void produce_kw(uint32_t w[16], uint4 (*slot)[64], uint32_t lane) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        uint32_t kw[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int j = 4 * q + i;
+            if (j >= 16) w[j & 15] += ssig1(w[(j - 2) & 15]) + w[(j - 7) & 15] + ssig0(w[(j - 15) & 15]);
+            kw[i] = kK[j] + w[j & 15];
+        }
+        slot[q][lane] = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+    }
+}
+
+// 64 rounds of one block from a ring slot; st += F only for a live block.
+__device__ __forceinline__ void consume_kw(uint4 (*slot)[64], uint32_t lane, uint32_t st[8], bool live) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = st[i];
+    uint4 a = slot[0][lane], b = slot[1][lane];
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        uint4 na = a, nb = b;
+        if (c < 7) {
+            na = slot[2 * c + 2][lane];
+            nb = slot[2 * c + 3][lane];
+        }
+        rounds_kw8_asm(s, a, b);
+        a = na;
+        b = nb;
+    }
+    if (live) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) st[i] += s[i];
+    }
+}
+
+__device__ __forceinline__ uint32_t ld_u32(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool live);
+__device__ __forceinline__ void load_digest(__amdgpu_buffer_rsrc_t rsrc, uint32_t id, bool live, uint4& x0,
+                                            uint4& x1);
+
+// Producer-side sources of block words, called for blocks 0, 1, 2, ... in
+// order; each keeps the next block's loads in flight.
+struct ArenaBlocks {  // message bytes at any alignment in an arena (< 4 GiB)
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t records, o, L, nb;
+    RawChunk cur[4];
+    __device__ void start(const uint8_t* arena, uint64_t arena_len, uint32_t off_, uint32_t L_, uint32_t nb_) {
+        records = (uint32_t)((arena_len + 3u) & ~3ull);
+        rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)records, 0x00020000);
+        o = off_;
+        L = L_;
+        nb = nb_;
+#pragma unroll
+        for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, 0u, (uint32_t)q, 0u < nb, cur[q]);
+    }
+    __device__ void block(uint32_t blk, uint32_t w[16]) {
+        RawChunk nxt[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, blk + 1u, (uint32_t)q, blk + 1u < nb, nxt[q]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) finish_chunk(cur[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) cur[q] = nxt[q];
+    }
+};
+
+struct ListBlocks {  // concat(digests[cidx[e]]) of a compacted list (no null entries)
+    __amdgpu_buffer_rsrc_t drs, irs;
+    uint32_t e0, c, L, nb;
+    uint4 cur[4];
+    uint32_t nx0, nx1;
+    __device__ void start(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
+                          uint32_t e0_, uint32_t c_, uint32_t nb_) {
+        drs = __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
+        irs = __builtin_amdgcn_make_buffer_rsrc((void*)cidx, (short)0, (int)(4u * n_entries), 0x00020000);
+        e0 = e0_;
+        c = c_;
+        L = 32u * c;
+        nb = nb_;
+        nx0 = ld_u32(irs, 4u * (e0 + 2u), 2u < c);
+        nx1 = ld_u32(irs, 4u * (e0 + 3u), 3u < c);
+        const uint32_t i0 = ld_u32(irs, 4u * e0, 0u < c), i1 = ld_u32(irs, 4u * (e0 + 1u), 1u < c);
+        load_digest(drs, i0, 0u < c, cur[0], cur[1]);
+        load_digest(drs, i1, 1u < c, cur[2], cur[3]);
+    }
+    __device__ void block(uint32_t blk, uint32_t w[16]) {
+        uint4 nxt[4];
+        load_digest(drs, nx0, 2u * blk + 2u < c, nxt[0], nxt[1]);
+        load_digest(drs, nx1, 2u * blk + 3u < c, nxt[2], nxt[3]);
+        const uint32_t nn0 = ld_u32(irs, 4u * (e0 + 2u * blk + 4u), 2u * blk + 4u < c);
+        const uint32_t nn1 = ld_u32(irs, 4u * (e0 + 2u * blk + 5u), 2u * blk + 5u < c);
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const uint32_t di = 2u * blk + (uint32_t)half;  // digest ordinal in the message
+            const uint4 x0 = cur[2 * half], x1 = cur[2 * half + 1];
+            // past the end the loads returned zeros; only the 0x80 marker is added
+            w[8 * half + 0] = __builtin_bswap32(x0.x) | (di == c ? 0x80000000u : 0u);
+            w[8 * half + 1] = __builtin_bswap32(x0.y); w[8 * half + 2] = __builtin_bswap32(x0.z);
+            w[8 * half + 3] = __builtin_bswap32(x0.w); w[8 * half + 4] = __builtin_bswap32(x1.x);
+            w[8 * half + 5] = __builtin_bswap32(x1.y); w[8 * half + 6] = __builtin_bswap32(x1.z);
+            w[8 * half + 7] = __builtin_bswap32(x1.w);
+        }
+        if (blk + 1u == nb) {
+            w[14] = L >> 29;
+            w[15] = L << 3;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) cur[i] = nxt[i];
+        nx0 = nn0;
+        nx1 = nn1;
+    }
+};
+
+// The pair loop shared by both sources: the producer stays one block ahead.
+template <class Src>
+__device__ __forceinline__ void pair_loop(Src& src, PairRing& ring, bool producer, uint32_t lane, uint32_t nb,
+                                          uint32_t st[8]) {
+    const uint32_t wave_nb = wave_max(nb);  // same in both waves: they serve the same 64 messages
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    if (producer && wave_nb) {
+        uint32_t w[16];
+        src.block(0u, w);
+        produce_kw(w, ring.kw[0], lane);
+    }
+    __syncthreads();
+    for (uint32_t blk = 0; blk < wave_nb; blk++) {
+        if (producer) {
+            if (blk + 1u < wave_nb) {
+                uint32_t w[16];
+                src.block(blk + 1u, w);
+                produce_kw(w, ring.kw[(blk + 1u) & 1u], lane);
+            }
+        } else {
+            consume_kw(ring.kw[blk & 1u], lane, st, blk < nb);
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kPairThreads) void sha256_msgs_pair_kernel(
+    const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
+    const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out) {
+    __shared__ PairRing ring;
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool producer = threadIdx.x < 64u;
+    const uint32_t slot = blockIdx.x * 64u + lane;
+    const bool valid = slot < n;
+    const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
+    const uint32_t L = valid ? len[msg] : 0u;
+    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
+    ArenaBlocks src;
+    if (producer) src.start(arena, arena_len, valid ? (uint32_t)off[msg] : 0u, L, nb);
+    uint32_t st[8];
+    pair_loop(src, ring, producer, lane, nb, st);
+    if (!producer && valid) store_digest(out, msg, st);
+}
+
+__global__ __launch_bounds__(kPairThreads) void sha256_chain_pair_kernel(
+    const uint8_t* __restrict__ digests, uint32_t n_digests, const uint32_t* __restrict__ cidx, uint32_t n_entries,
+    const uint32_t* __restrict__ cfirst, uint32_t n_lists, uint8_t* __restrict__ out) {
+    __shared__ PairRing ring;
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool producer = threadIdx.x < 64u;
+    const uint32_t k = blockIdx.x * 64u + lane;
+    const bool valid = k < n_lists;
+    const uint32_t e0 = valid ? cfirst[k] : 0u;
+    const uint32_t c = valid ? cfirst[k + 1] - e0 : 0u;
+    const uint32_t nb = valid ? blocks_for_len(32u * c) : 0u;
+    ListBlocks src;
+    if (producer) src.start(digests, n_digests, cidx, n_entries, e0, c, nb);
+    uint32_t st[8];
+    pair_loop(src, ring, producer, lane, nb, st);
+    if (!producer && valid) store_digest(out, k, st);
+}
+
 // Dependent pass: message k = concat(digests[idx[e]] for e in [first[k], first[k+1]))
 // skipping idx == kNullIndex (a null request's empty digest, client_tracker.go:840-847).
 // One lane per list.  These waves run few per SIMD, so every global read on
@@ -825,6 +1022,14 @@ __global__ void gen_mixed_kernel(uint64_t seed, uint64_t first, uint64_t count, 
 }
 
 // ---- host-side launchers --------------------------------------------------
+bool pairs_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("MIRSHA_PAIR");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
                        const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
                        int variant, hipStream_t s) {
@@ -833,6 +1038,10 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
     const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
     if (arena_len > kMaxBufferArena) {  // 64-bit per-lane addressing (LDS loader, asm rounds)
         sha256_msgs_kernel<true, true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        return hipGetLastError();
+    }
+    if (variant == kVariantPair || (variant == kVariantLds && tiles <= kPairMaxGroups && pairs_enabled())) {
+        sha256_msgs_pair_kernel<<<tiles, kPairThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantLowOcc || (variant == kVariantLds && tiles <= kLowOccTiles)) {
@@ -873,6 +1082,14 @@ hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32
     const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
     sha256_chain_kernel<<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists, ob, oe,
                                                       state, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
+                             const uint32_t* cfirst, uint32_t n_lists, uint8_t* out, hipStream_t s) {
+    if (n_lists == 0) return hipSuccess;
+    const uint32_t groups = (n_lists + 63u) / 64u;
+    sha256_chain_pair_kernel<<<groups, kPairThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists, out);
     return hipGetLastError();
 }
 

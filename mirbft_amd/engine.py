@@ -34,6 +34,7 @@ VARIANT_LDS_CXX = 2
 VARIANT_DIRECT_CXX = 3
 VARIANT_LOWOCC = 4
 VARIANT_LDS_ONLY = 5
+VARIANT_PAIR = 6
 
 
 def _ptr(a: np.ndarray | None) -> int | None:
@@ -418,4 +419,5 @@ __all__ = [
     "VARIANT_DIRECT",
     "VARIANT_LOWOCC",
     "VARIANT_LDS_ONLY",
+    "VARIANT_PAIR",
 ]

@@ -15,7 +15,7 @@ from mirbft_amd import (ActionResults, Actions, Engine, HashRequest, MirshaError
                         gpu_hasher, hash_batch_multi, hashdata, sharding)
 from mirbft_amd import _lib
 from mirbft_amd.engine import (KERNEL_LISTS, KERNEL_MSGS, VARIANT_DIRECT, VARIANT_DIRECT_CXX, VARIANT_LDS,
-                               VARIANT_LDS_CXX, VARIANT_LDS_ONLY, VARIANT_LOWOCC)
+                               VARIANT_LDS_CXX, VARIANT_LDS_ONLY, VARIANT_LOWOCC, VARIANT_PAIR)
 
 pytestmark = pytest.mark.gpu
 
@@ -23,8 +23,8 @@ EMPTY = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 
 
 @pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LDS_CXX, VARIANT_DIRECT_CXX, VARIANT_LOWOCC,
-                        VARIANT_LDS_ONLY],
-                ids=["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only"])
+                        VARIANT_LDS_ONLY, VARIANT_PAIR],
+                ids=["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only", "pair"])
 def eng(engine, request):
     engine.set_variant(request.param)
     yield engine
