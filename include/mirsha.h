@@ -257,6 +257,27 @@ int mirsha_hash_requests_then_batches_device(mirsha_ctx* ctx, mirsha_pipeline* p
  * Returns 1 if the order is the identity (all lengths in one bucket), else 0. */
 int mirsha_bucket_order(const uint32_t* len, uint32_t n, uint32_t* order_out);
 
+/* ------------------------------------- streaming checkpoint chains (f4) */
+/* Device-resident running SHA-256 states, one per application node: the
+ * testengine application's checkpoint value is Sum() of a hash into which
+ * every committed request digest is written (NodeState.Commit,
+ * testengine/recorder.go:213-256: ActiveHash.Write :223, Sum :244) and which
+ * restarts at each checkpoint (NodeState.Set, :186-207).
+ *   mirsha_chains_absorb: ActiveHash.Write(digest) for m 32-byte digests, in
+ *     order; digest i goes to chain chain_of[i].  A null request's digest is
+ *     empty and its Write changes nothing: leave it out.
+ *   mirsha_chains_sum: ActiveHash.Sum(nil) of chains which[0..k) into
+ *     out[32*j]; like Go's Sum it leaves the states unchanged.
+ *   mirsha_chains_reset: ActiveHash = Hasher() for chains which[0..k).
+ * Synchronous; chain ids < n_chains (else MIRSHA_EINVAL). */
+typedef struct mirsha_chains mirsha_chains;
+int mirsha_chains_create(mirsha_ctx* ctx, uint32_t n_chains, mirsha_chains** out);
+void mirsha_chains_destroy(mirsha_chains* chains);
+int mirsha_chains_absorb(mirsha_ctx* ctx, mirsha_chains* chains, const uint8_t* digests, const uint32_t* chain_of,
+                         uint32_t m);
+int mirsha_chains_sum(mirsha_ctx* ctx, mirsha_chains* chains, const uint32_t* which, uint32_t k, uint8_t* out);
+int mirsha_chains_reset(mirsha_ctx* ctx, mirsha_chains* chains, const uint32_t* which, uint32_t k);
+
 /* ------------------------------------------------- multi-GPU (one process) */
 /* Shards the n requests by contiguous range across ndev devices (balanced by
  * block count), one context per device, host gather into origin order.  No

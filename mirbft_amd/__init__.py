@@ -7,12 +7,13 @@ hand-written gfx950 HIP kernels behind the C-ABI in include/mirsha.h.
 """
 from . import hashdata, sharding
 from ._lib import MirshaError, MirshaUnavailable
-from .engine import Engine, SliceArrays, Ticket, bucket_order, dedup_plan, device_count, hash_batch_multi
+from .engine import CheckpointChains, Engine, SliceArrays, Ticket, bucket_order, dedup_plan, device_count, hash_batch_multi
 from .processor import (ActionResults, Actions, GpuHash, HashRequest, HashResult, PendingResults, Processor,
                         ProcessorWorkPool, gpu_hasher)
 
 __all__ = [
     "Engine",
+    "CheckpointChains",
     "SliceArrays",
     "Ticket",
     "dedup_plan",

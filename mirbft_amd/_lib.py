@@ -84,6 +84,11 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "mirsha_chains_create": (c_int, [c_void_p, c_uint32, POINTER(c_void_p)]),
+    "mirsha_chains_destroy": (None, [c_void_p]),
+    "mirsha_chains_absorb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),
+    "mirsha_chains_sum": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
+    "mirsha_chains_reset": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32]),
     "mirsha_hash_batch_multi": (
         c_int,
         [c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p],

@@ -109,6 +109,14 @@ struct mirsha_ctx {
     uint64_t done_ticket = 0;  // every ticket <= this one has completed
 };
 
+// Streaming checkpoint chains (see mirsha.h, mirsha_chains_create).
+struct mirsha_chains {
+    int device = 0;
+    uint32_t n = 0;
+    DevBuf d_h, d_pend, d_cnt;                        // state
+    DevBuf d_dig, d_pos, d_act, d_afirst, d_which, d_out;  // per call
+};
+
 // A request -> batch-digest pipeline plan (see mirsha.h, mirsha_pipeline_create).
 struct mirsha_pipeline {
     int device = 0;
@@ -1314,6 +1322,128 @@ int mirsha_synth_requests_device(mirsha_ctx* c, uint64_t seed, uint64_t first, u
     if (count && !d_arena) return fail(c, MIRSHA_EINVAL, "NULL arena");
     if (int rc = use_device(c)) return rc;
     return timed_launch(c, 2, [&] { return mirsha::launch_gen_requests(seed, first, count, data_len, d_arena, c->stream); });
+}
+
+int mirsha_chains_create(mirsha_ctx* c, uint32_t n, mirsha_chains** out) {
+    if (!c || !out) return MIRSHA_EINVAL;
+    *out = nullptr;
+    if (n == 0) return fail(c, MIRSHA_EINVAL, "n_chains must be > 0");
+    if (int rc = use_device(c)) return rc;
+    auto* ch = new mirsha_chains();
+    ch->device = c->device;
+    ch->n = n;
+    std::vector<uint32_t> h(8ull * n);
+    for (uint32_t i = 0; i < n; i++)
+        for (int j = 0; j < 8; j++) h[8ull * i + j] = mirsha::kH0[j];
+    auto up = [&]() -> int {
+        HIP_TRY(c, ch->d_h.ensure(32ull * n));
+        HIP_TRY(c, ch->d_pend.ensure(32ull * n));
+        HIP_TRY(c, ch->d_cnt.ensure(8ull * n));
+        HIP_TRY(c, hipMemcpy(ch->d_h.p, h.data(), 32ull * n, hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemset(ch->d_pend.p, 0, 32ull * n));
+        HIP_TRY(c, hipMemset(ch->d_cnt.p, 0, 8ull * n));
+        return MIRSHA_OK;
+    };
+    if (int rc = up()) {
+        mirsha_chains_destroy(ch);
+        return rc;
+    }
+    *out = ch;
+    return MIRSHA_OK;
+}
+
+void mirsha_chains_destroy(mirsha_chains* ch) {
+    if (!ch) return;
+    (void)hipSetDevice(ch->device);
+    for (DevBuf* b : {&ch->d_h, &ch->d_pend, &ch->d_cnt, &ch->d_dig, &ch->d_pos, &ch->d_act, &ch->d_afirst,
+                      &ch->d_which, &ch->d_out})
+        b->release();
+    delete ch;
+}
+
+int mirsha_chains_absorb(mirsha_ctx* c, mirsha_chains* ch, const uint8_t* digests, const uint32_t* chain_of,
+                         uint32_t m) {
+    if (!c || !ch) return MIRSHA_EINVAL;
+    if (m == 0) return MIRSHA_OK;
+    if (!digests || !chain_of) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (ch->device != c->device) return fail(c, MIRSHA_EINVAL, "chains belong to another device");
+    // Group the writes by chain, keeping their order (counting sort).
+    std::vector<uint32_t> count(ch->n + 1, 0);
+    for (uint32_t i = 0; i < m; i++) {
+        if (chain_of[i] >= ch->n) return fail(c, MIRSHA_EINVAL, "chain_of[%u] = %u >= %u", i, chain_of[i], ch->n);
+        count[chain_of[i] + 1]++;
+    }
+    std::vector<uint32_t> act, afirst(1, 0);
+    for (uint32_t k = 0; k < ch->n; k++)
+        if (count[k + 1]) {
+            act.push_back(k);
+            afirst.push_back(afirst.back() + count[k + 1]);
+        }
+    for (uint32_t k = 0; k < ch->n; k++) count[k + 1] += count[k];
+    std::vector<uint32_t> pos(m);
+    for (uint32_t i = 0; i < m; i++) pos[count[chain_of[i]]++] = i;
+    if (int rc = use_device(c)) return rc;
+    const uint32_t na = (uint32_t)act.size();
+    HIP_TRY(c, ch->d_dig.ensure(32ull * m));
+    HIP_TRY(c, ch->d_pos.ensure(4ull * m));
+    HIP_TRY(c, ch->d_act.ensure(4ull * na));
+    HIP_TRY(c, ch->d_afirst.ensure(4ull * (na + 1)));
+    HIP_TRY(c, hipMemcpyAsync(ch->d_dig.p, digests, 32ull * m, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(ch->d_pos.p, pos.data(), 4ull * m, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(ch->d_act.p, act.data(), 4ull * na, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(ch->d_afirst.p, afirst.data(), 4ull * (na + 1), hipMemcpyHostToDevice, c->stream));
+    if (int rc = timed_launch(c, 1, [&] {
+            return mirsha::launch_chains_absorb(ch->d_dig.as<uint8_t>(), ch->d_pos.as<uint32_t>(),
+                                                ch->d_act.as<uint32_t>(), ch->d_afirst.as<uint32_t>(), na,
+                                                ch->d_h.as<uint32_t>(), ch->d_pend.as<uint32_t>(),
+                                                ch->d_cnt.as<uint64_t>(), c->stream);
+        }))
+        return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors above feed async copies
+    return MIRSHA_OK;
+}
+
+namespace {
+int chains_which(mirsha_ctx* c, mirsha_chains* ch, const uint32_t* which, uint32_t k) {
+    if (!which) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (ch->device != c->device) return fail(c, MIRSHA_EINVAL, "chains belong to another device");
+    for (uint32_t j = 0; j < k; j++)
+        if (which[j] >= ch->n) return fail(c, MIRSHA_EINVAL, "which[%u] = %u >= %u", j, which[j], ch->n);
+    if (int rc = use_device(c)) return rc;
+    HIP_TRY(c, ch->d_which.ensure(4ull * k));
+    HIP_TRY(c, hipMemcpyAsync(ch->d_which.p, which, 4ull * k, hipMemcpyHostToDevice, c->stream));
+    return MIRSHA_OK;
+}
+}  // namespace
+
+int mirsha_chains_sum(mirsha_ctx* c, mirsha_chains* ch, const uint32_t* which, uint32_t k, uint8_t* out) {
+    if (!c || !ch) return MIRSHA_EINVAL;
+    if (k == 0) return MIRSHA_OK;
+    if (!out) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (int rc = chains_which(c, ch, which, k)) return rc;
+    HIP_TRY(c, ch->d_out.ensure(32ull * k));
+    if (int rc = timed_launch(c, 1, [&] {
+            return mirsha::launch_chains_sum(ch->d_which.as<uint32_t>(), k, ch->d_h.as<uint32_t>(),
+                                             ch->d_pend.as<uint32_t>(), ch->d_cnt.as<uint64_t>(),
+                                             ch->d_out.as<uint8_t>(), c->stream);
+        }))
+        return rc;
+    HIP_TRY(c, hipMemcpyAsync(out, ch->d_out.p, 32ull * k, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_chains_reset(mirsha_ctx* c, mirsha_chains* ch, const uint32_t* which, uint32_t k) {
+    if (!c || !ch) return MIRSHA_EINVAL;
+    if (k == 0) return MIRSHA_OK;
+    if (int rc = chains_which(c, ch, which, k)) return rc;
+    if (int rc = timed_launch(c, 1, [&] {
+            return mirsha::launch_chains_reset(ch->d_which.as<uint32_t>(), k, ch->d_h.as<uint32_t>(),
+                                               ch->d_cnt.as<uint64_t>(), c->stream);
+        }))
+        return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
 }
 
 int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena, uint64_t arena_len,

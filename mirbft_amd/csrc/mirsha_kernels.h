@@ -83,6 +83,13 @@ struct FusedArgs {
 // (kPacedLds of reserved LDS), `pace` tile waves per SIMD in tile blocks.
 constexpr uint32_t kPacedLds = 96u * 1024u;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
+// Streaming checkpoint chains (state: midstate h[8], pending digest words
+// pend[8], digest count cnt per chain), see mirsha_kernels.hip.
+hipError_t launch_chains_absorb(const uint8_t* digests, const uint32_t* pos, const uint32_t* act, const uint32_t* afirst,
+                                uint32_t n_active, uint32_t* h, uint32_t* pend, uint64_t* cnt, hipStream_t s);
+hipError_t launch_chains_sum(const uint32_t* which, uint32_t k, const uint32_t* h, const uint32_t* pend,
+                             const uint64_t* cnt, uint8_t* out, hipStream_t s);
+hipError_t launch_chains_reset(const uint32_t* which, uint32_t k, uint32_t* h, uint64_t* cnt, hipStream_t s);
 hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t data_len,
                                uint8_t* arena, hipStream_t s);
 hipError_t launch_mixed_lengths(uint64_t seed, uint64_t first, uint64_t count, uint32_t* len, hipStream_t s);

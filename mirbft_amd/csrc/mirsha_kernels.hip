@@ -1113,6 +1113,139 @@ hipError_t launch_mixed_lengths(uint64_t seed, uint64_t first, uint64_t count, u
     return hipGetLastError();
 }
 
+// ---- streaming checkpoint chains (testengine NodeState.ActiveHash) ---------
+// Running SHA-256 states, one per application node: the checkpoint value of
+// testengine/recorder.go:213-256 is Sum() of a hash that every committed
+// request digest is written into (ActiveHash.Write, :223), reset at each
+// checkpoint (Set, :187).  State per chain: midstate h[8], the pending
+// digest of an odd count (its 8 big-endian words) and the digest count.
+// Writes are 32-byte digests, so a block is always two whole digests.
+__device__ __forceinline__ void load_digest_words(const uint8_t* __restrict__ digests, uint32_t p, bool live,
+                                                  uint32_t w[8]) {
+    if (live) {
+        const uint4* d = reinterpret_cast<const uint4*>(digests + 32ull * p);
+        const uint4 a = d[0], b = d[1];
+        w[0] = __builtin_bswap32(a.x); w[1] = __builtin_bswap32(a.y);
+        w[2] = __builtin_bswap32(a.z); w[3] = __builtin_bswap32(a.w);
+        w[4] = __builtin_bswap32(b.x); w[5] = __builtin_bswap32(b.y);
+        w[6] = __builtin_bswap32(b.z); w[7] = __builtin_bswap32(b.w);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; i++) w[i] = 0u;
+    }
+}
+
+// One lane per chain with new digests pos[afirst[k] .. afirst[k+1]) (in write
+// order).  With `odd` = a digest pending from earlier writes, the lane
+// completes (odd + m) / 2 blocks: block t = digest q ‖ digest q+1 with
+// q = 2t - odd (q = -1: the pending digest).
+__global__ __launch_bounds__(kBlockThreads) void chains_absorb_kernel(
+    const uint8_t* __restrict__ digests, const uint32_t* __restrict__ pos, const uint32_t* __restrict__ act,
+    const uint32_t* __restrict__ afirst, uint32_t n_active, uint32_t* __restrict__ h, uint32_t* __restrict__ pend,
+    uint64_t* __restrict__ cnt) {
+    const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
+    const bool valid = k < n_active;
+    const uint32_t c = valid ? act[k] : 0u;
+    const uint32_t e0 = valid ? afirst[k] : 0u;
+    const uint32_t m = valid ? afirst[k + 1] - e0 : 0u;
+    uint32_t st[8], pw[8];
+    uint64_t n = 0;
+    if (valid) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            st[i] = h[8ull * c + i];
+            pw[i] = pend[8ull * c + i];
+        }
+        n = cnt[c];
+    }
+    const uint32_t odd = (uint32_t)(n & 1u);
+    const uint32_t blocks = (odd + m) / 2u;
+    const uint32_t steps = wave_max(blocks);
+    for (uint32_t t = 0; t < steps; t++) {
+        const bool live = t < blocks;
+        const int32_t q = (int32_t)(2u * t) - (int32_t)odd;
+        uint32_t w[16];
+        if (q < 0) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) w[i] = pw[i];
+        } else {
+            load_digest_words(digests, pos[e0 + (uint32_t)q], live, w);
+        }
+        load_digest_words(digests, live ? pos[e0 + (uint32_t)(q + 1)] : 0u, live, w + 8);
+        if (live) compress_asm_lat(st, w);
+    }
+    if (valid) {
+        if ((odd + m) & 1u) {
+            if (m) load_digest_words(digests, pos[e0 + m - 1u], true, pw);  // else the old pending stays
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            h[8ull * c + i] = st[i];
+            pend[8ull * c + i] = pw[i];
+        }
+        cnt[c] = n + m;
+    }
+}
+
+// Sum(nil) of chains which[0..k): the final padded block (pending digest, if
+// any, then 0x80 and the 64-bit bit length) from a copy of the midstate.
+__global__ __launch_bounds__(kBlockThreads) void chains_sum_kernel(const uint32_t* __restrict__ which, uint32_t k_n,
+                                                                   const uint32_t* __restrict__ h,
+                                                                   const uint32_t* __restrict__ pend,
+                                                                   const uint64_t* __restrict__ cnt,
+                                                                   uint8_t* __restrict__ out) {
+    const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
+    const bool valid = k < k_n;
+    const uint32_t c = valid ? which[k] : 0u;
+    uint32_t st[8], w[16];
+    const uint64_t n = valid ? cnt[c] : 0u;
+    const bool odd = (n & 1u) != 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        st[i] = valid ? h[8ull * c + i] : 0u;
+        w[i] = odd ? pend[8ull * c + i] : 0u;
+        w[8 + i] = 0u;
+    }
+    w[odd ? 8 : 0] = 0x80000000u;
+    const uint64_t bits = n * 256u;
+    w[14] = (uint32_t)(bits >> 32);
+    w[15] = (uint32_t)bits;
+    compress_asm_lat(st, w);
+    if (valid) store_digest(out, k, st);
+}
+
+__global__ __launch_bounds__(kBlockThreads) void chains_reset_kernel(const uint32_t* __restrict__ which, uint32_t k_n,
+                                                                     uint32_t* __restrict__ h,
+                                                                     uint64_t* __restrict__ cnt) {
+    const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
+    if (k >= k_n) return;
+    const uint32_t c = which[k];
+#pragma unroll
+    for (int i = 0; i < 8; i++) h[8ull * c + i] = kH0[i];
+    cnt[c] = 0u;
+}
+
+hipError_t launch_chains_absorb(const uint8_t* digests, const uint32_t* pos, const uint32_t* act, const uint32_t* afirst,
+                                uint32_t n_active, uint32_t* h, uint32_t* pend, uint64_t* cnt, hipStream_t s) {
+    if (n_active == 0) return hipSuccess;
+    chains_absorb_kernel<<<(n_active + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s>>>(
+        digests, pos, act, afirst, n_active, h, pend, cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_chains_sum(const uint32_t* which, uint32_t k, const uint32_t* h, const uint32_t* pend,
+                             const uint64_t* cnt, uint8_t* out, hipStream_t s) {
+    if (k == 0) return hipSuccess;
+    chains_sum_kernel<<<(k + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s>>>(which, k, h, pend, cnt, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_chains_reset(const uint32_t* which, uint32_t k, uint32_t* h, uint64_t* cnt, hipStream_t s) {
+    if (k == 0) return hipSuccess;
+    chains_reset_kernel<<<(k + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s>>>(which, k, h, cnt);
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_mixed(uint64_t seed, uint64_t first, uint64_t count, const uint64_t* off, uint8_t* arena,
                             hipStream_t s) {
     if (count == 0) return hipSuccess;

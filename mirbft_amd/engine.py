@@ -374,6 +374,55 @@ class Pipeline:
             pass
 
 
+class CheckpointChains:
+    """Streaming checkpoint chains on the device (mirsha_chains_*): one running
+    SHA-256 per application node, as testengine's NodeState.ActiveHash
+    (testengine/recorder.go:186-256).  write() = ActiveHash.Write of committed
+    request digests, sum() = ActiveHash.Sum(nil) (state unchanged),
+    reset() = NodeState.Set's fresh hasher."""
+
+    def __init__(self, engine: Engine, n_chains: int):
+        self._engine = engine
+        self._lib = engine._lib
+        h = ctypes.c_void_p()
+        engine._check(self._lib.mirsha_chains_create(engine.ctx, int(n_chains), ctypes.byref(h)))
+        self.handle = h
+        self.n = int(n_chains)
+
+    def write(self, digests, chain_of) -> None:
+        d = np.ascontiguousarray(digests, dtype=np.uint8).reshape(-1, 32)
+        c = np.ascontiguousarray(chain_of, dtype=np.uint32).reshape(-1)
+        if c.size != d.shape[0]:
+            raise ValueError("one chain id per digest")
+        if c.size:
+            self._engine._check(self._lib.mirsha_chains_absorb(self._engine.ctx, self.handle, _ptr(d), _ptr(c),
+                                                               c.size))
+
+    def sum(self, which) -> np.ndarray:
+        w = np.ascontiguousarray(which, dtype=np.uint32).reshape(-1)
+        out = np.empty((w.size, 32), dtype=np.uint8)
+        if w.size:
+            self._engine._check(self._lib.mirsha_chains_sum(self._engine.ctx, self.handle, _ptr(w), w.size,
+                                                            _ptr(out)))
+        return out
+
+    def reset(self, which) -> None:
+        w = np.ascontiguousarray(which, dtype=np.uint32).reshape(-1)
+        if w.size:
+            self._engine._check(self._lib.mirsha_chains_reset(self._engine.ctx, self.handle, _ptr(w), w.size))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.mirsha_chains_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def bucket_order(length: Sequence[int]) -> tuple[np.ndarray, bool]:
     """Message order sorted by block count, longest first (stable); (order, is_identity)."""
     ln = np.ascontiguousarray(length, dtype=np.uint32)
@@ -398,6 +447,7 @@ def hash_batch_multi(devices: Iterable[int], arena, off, length) -> np.ndarray:
 
 __all__ = [
     "Engine",
+    "CheckpointChains",
     "SliceArrays",
     "Ticket",
     "dedup_plan",
