@@ -487,7 +487,7 @@ int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint
                 }))
                 return rc;
         }
-        if (mirsha::pairs_enabled() && (p->n_lists + 63u) / 64u <= mirsha::kPairMaxGroups)
+        if ((p->n_lists + 63u) / 64u <= mirsha::pair_max_groups())
             return timed_launch(c, 1, [&] {  // few long chains: producer/consumer pairs
                 return mirsha::launch_chain_pair(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
                                                  p->d_cfirst.as<uint32_t>(), p->n_lists, d_list_out, c->stream);

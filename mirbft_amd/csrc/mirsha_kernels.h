@@ -24,11 +24,13 @@ enum : int {
     kVariantPair = 6
 };
 constexpr uint32_t kLowOccTiles = 1024;   // 256 CUs x 4 SIMDs
-// Small launches take a latency form: at most kPairMaxGroups 64-message groups
-// the producer/consumer pair kernels (<= 2 pairs per CU: every wave alone on
-// a SIMD).  MIRSHA_PAIR=0 in the environment turns the automatic choice off.
+// Small launches take a latency form: at most pair_max_groups() 64-message
+// groups (default kPairMaxGroups: <= 2 pairs per CU, every wave alone on a
+// SIMD) the producer/consumer pair kernels.  Environment (A/B):
+// MIRSHA_PAIR=0 turns the automatic choice off, MIRSHA_PAIR_MAX_GROUPS=n
+// moves the threshold.
 constexpr uint32_t kPairMaxGroups = 512;
-bool pairs_enabled();
+uint32_t pair_max_groups();
 
 // Arenas up to kMaxBufferArena bytes use one 32-bit buffer descriptor; larger
 // ones (any size) the 64-bit per-lane addressed loader.

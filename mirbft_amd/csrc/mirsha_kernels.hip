@@ -1022,12 +1022,14 @@ __global__ void gen_mixed_kernel(uint64_t seed, uint64_t first, uint64_t count, 
 }
 
 // ---- host-side launchers --------------------------------------------------
-bool pairs_enabled() {
-    static const bool on = [] {
+uint32_t pair_max_groups() {
+    static const uint32_t v = [] {
         const char* e = getenv("MIRSHA_PAIR");
-        return !(e && e[0] == '0');
+        if (e && e[0] == '0') return 0u;
+        const char* m = getenv("MIRSHA_PAIR_MAX_GROUPS");
+        return m ? (uint32_t)strtoul(m, nullptr, 10) : kPairMaxGroups;
     }();
-    return on;
+    return v;
 }
 
 hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
@@ -1040,7 +1042,7 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_kernel<true, true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
-    if (variant == kVariantPair || (variant == kVariantLds && tiles <= kPairMaxGroups && pairs_enabled())) {
+    if (variant == kVariantPair || (variant == kVariantLds && tiles <= pair_max_groups())) {
         sha256_msgs_pair_kernel<<<tiles, kPairThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
