@@ -126,6 +126,7 @@ struct mirsha_pipeline {
     std::vector<uint32_t> tadj_first, tadj, cbase, expected;
     uint32_t n_tiles = 0, n_groups = 0, n_counters = 0, grid = 0;
     uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
+    uint32_t fused_flags = 0;                             // mirsha::kFusedTile* (MIRSHA_FUSED_FLAGS)
     uint64_t tile_base = 0, list_base = 0;
     uint32_t epoch = 0;
     DevBuf d_tadj_first, d_tadj, d_cbase, d_expected, d_counters, d_ctl, d_trace;
@@ -607,6 +608,8 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
     const uint32_t cus = (uint32_t)prop.multiProcessorCount;
     p->pace = 1;
+    if (const char* e = getenv("MIRSHA_FUSED_PACE")) p->pace = std::min<uint32_t>(2u, std::max<uint32_t>(1u, (uint32_t)atoi(e)));
+    if (const char* e = getenv("MIRSHA_FUSED_FLAGS")) p->fused_flags = (uint32_t)atoi(e);
     const uint32_t lw = std::min<uint32_t>(p->n_groups, kFusedMaxListWaves);
     p->list_blocks = std::min<uint32_t>((lw + 3u) / 4u, cus / 4u);
     const uint32_t tile_blocks =
@@ -672,6 +675,7 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.n_tiles = p->n_tiles;
     a.n_groups = p->n_groups;
     a.list_waves = p->list_blocks;
+    a.flags = p->fused_flags;
     if (int rc = timed_launch(c, 4, [&] { return mirsha::launch_fused_paced(a, p->grid, p->pace, c->stream); }))
         return rc;
     // Tile waves and list waves each made exactly one failing claim on their ticket.

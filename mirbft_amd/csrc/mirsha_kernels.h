@@ -80,7 +80,10 @@ struct FusedArgs {
     unsigned long long tile_base, list_base;
     uint32_t arena_len, n_req, n_entries, n_lists;
     uint32_t epoch, n_tiles, n_groups, list_waves;
+    uint32_t flags;  // kFusedTilePrio | kFusedTileYield (A/B knobs, MIRSHA_FUSED_FLAGS)
 };
+constexpr uint32_t kFusedTilePrio = 1;   // s_setprio 2/1/0 for tiles by ticket third (early tiles first)
+constexpr uint32_t kFusedTileYield = 2;  // issue-yield rounds in tile waves (pace >= 2)
 // list_waves = number of list BLOCKS (first in the grid); one block per CU
 // (kPacedLds of reserved LDS), `pace` tile waves per SIMD in tile blocks.
 constexpr uint32_t kPacedLds = 96u * 1024u;

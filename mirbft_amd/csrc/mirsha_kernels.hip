@@ -880,6 +880,7 @@ __device__ __forceinline__ void fused_list_group_deep(const FusedArgs& a, __amdg
 // Tile loader prefetching kTileDepth blocks ahead (paced kernel: a tile wave is
 // alone on its SIMD, and a load under full request load takes several us).
 constexpr int kTileDepth = 3;
+template <bool kYield>
 __device__ __forceinline__ void hash_tile_deep(const uint8_t* __restrict__ arena, uint32_t arena_len,
                                                const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                                const uint32_t* __restrict__ order, uint32_t n,
@@ -913,7 +914,12 @@ __device__ __forceinline__ void hash_tile_deep(const uint8_t* __restrict__ arena
         const uint32_t nbk = blk + (uint32_t)kTileDepth;
 #pragma unroll
         for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, nbk, (uint32_t)q, nbk < nb, rc[kTileDepth - 1][q]);
-        if (blk < nb) compress_asm_lat(st, w);
+        if (blk < nb) {
+            if constexpr (kYield)
+                compress_asm(st, w);
+            else
+                compress_asm_lat(st, w);
+        }
     }
     if (valid) store_digest_sc1(ors, msg, st);
 }
@@ -945,7 +951,19 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
         const uint64_t t = claim(a.ctl + kCtlTileTicket, lane) - a.tile_base;
         if (t >= a.n_tiles) break;
         if (a.trace && lane == 0) a.trace[2 * t] = __builtin_amdgcn_s_memrealtime();
-        hash_tile_deep(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, drs, (uint32_t)t, lane);
+        if (a.flags & kFusedTilePrio) {  // early tickets feed the chains first: let them win issue
+            const uint32_t third = (uint32_t)((3ull * t) / a.n_tiles);
+            if (third == 0)
+                __builtin_amdgcn_s_setprio(2);
+            else if (third == 1)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
+        if (a.flags & kFusedTileYield)
+            hash_tile_deep<true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, drs, (uint32_t)t, lane);
+        else
+            hash_tile_deep<false>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, drs, (uint32_t)t, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (a.trace && lane == 0) a.trace[2 * t + 1] = __builtin_amdgcn_s_memrealtime();
         const uint32_t j0 = a.tadj_first[t], j1 = a.tadj_first[t + 1];

@@ -111,6 +111,49 @@ def any_then_dep(a, b):
     return operands(a)[0] in operands(b)[1]
 
 
+def insert_after(lines, mnemonics, filler):
+    out = []
+    for ln in lines:
+        out.append(ln)
+        if ln.split()[0] in mnemonics:
+            out.append(filler)
+    return out
+
+
+def interleave_cs(lines):
+    """Greedy reorder inside one block: after a complex op prefer an
+    independent simple op whose inputs are ready (dependencies respected)."""
+    remaining = list(lines)
+    out = []
+    written = {}
+    def deps(ln):
+        d, srcs = operands(ln)
+        return d, srcs
+    while remaining:
+        # candidates: instructions with no unsatisfied dependency on earlier remaining ones
+        pick = None
+        last_c = bool(out) and cls(out[-1]) == "C"
+        for i, ln in enumerate(remaining):
+            d, srcs = deps(ln)
+            blocked = False
+            for prev in remaining[:i]:
+                pd, ps = deps(prev)
+                if pd in srcs or d in ps or pd == d:
+                    blocked = True
+                    break
+            if blocked:
+                continue
+            if pick is None:
+                pick = i
+            if last_c and cls(ln) == "S":
+                pick = i
+                break
+            if not last_c:
+                break
+        out.append(remaining.pop(pick))
+    return out
+
+
 def ilp_block(j0):
     return remap_base(g.block_ilp(j0), kfirst=36)
 
@@ -187,6 +230,12 @@ SNOP = "s_nop 0"
 
 VARIANTS = [
     ("base", lambda j0: base_block(j0)),
+    ("snop_after_align", lambda j0: insert_after(base_block(j0), ("v_alignbit_b32",), SNOP)),
+    ("snop_after_add3", lambda j0: insert_after(base_block(j0), ("v_add3_u32",), SNOP)),
+    ("sleep0_after_c", lambda j0: insert(base_block(j0), "afterC", "s_sleep 0")),
+    ("setprio_after_c", lambda j0: insert(base_block(j0), "afterC", "s_setprio 0")),
+    ("interleave_snop_after_c", lambda j0: insert(interleave_cs(base_block(j0)), "afterC", SNOP)),
+    ("interleave", lambda j0: interleave_cs(base_block(j0))),
     ("snop_after_c", lambda j0: insert(base_block(j0), "afterC", SNOP)),
     ("snop1_after_c", lambda j0: insert(base_block(j0), "afterC", "s_nop 1")),
     ("snop_c_dep", lambda j0: insert_cond(base_block(j0), c_then_dep)),
