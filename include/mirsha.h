@@ -80,7 +80,9 @@ void* mirsha_ctx_stream(mirsha_ctx* ctx);
  *     MIRSHA_PAIR=0 in the environment disables the pair forms),
  * 1 = direct per-lane loads + asm rounds, 2 = LDS loader + compiler-scheduled
  * C++ rounds, 3 = direct loads + C++ rounds, 4 = the low-occupancy kernel at
- * any size, 5 = the LDS kernel at any size, 6 = the pair kernel at any size.
+ * any size, 5 = the LDS kernel at any size, 6 = the pair kernel at any size,
+ * 7 = LDS loader with the next block's loads in flight during the rounds,
+ * 8 = the round-1 LDS loader (per-chunk activity/range tests, 72 VGPRs).
  * All are bit-exact. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
@@ -132,6 +134,14 @@ int mirsha_hash_slices_dedup(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
 int mirsha_dedup_plan(const uint8_t* const* slice_ptr, const uint64_t* slice_len,
                       const uint32_t* slice_first, uint32_t n, uint32_t* rep_out,
                       uint32_t* n_unique_out);
+
+/* Page-locked host memory for the caller's request arena.  The cgo binding
+ * packs each Ready() cycle's request bytes into one C arena before the call
+ * (INTEGRATION.md); allocated here (once, reused every cycle) that arena is
+ * DMA'd to the GPU at PCIe rate, where a malloc'ed one goes through the
+ * runtime's pageable staging.  mirsha_host_free releases it. */
+int mirsha_host_alloc(mirsha_ctx* ctx, uint64_t bytes, void** out);
+void mirsha_host_free(void* p);
 
 /* ---------------------------------------- asynchronous, order-preserving */
 /* Replaces the hash stage of ProcessorWorkPool (processor.go:312-361,

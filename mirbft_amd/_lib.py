@@ -52,6 +52,8 @@ SIGNATURES = {
     "mirsha_hash_slices": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
     "mirsha_hash_slices_dedup": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, _u32p]),
     "mirsha_dedup_plan": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, _u32p]),
+    "mirsha_host_alloc": (c_int, [c_void_p, c_uint64, POINTER(c_void_p)]),
+    "mirsha_host_free": (None, [c_void_p]),
     "mirsha_submit_slices": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_int, _u64p]),
     "mirsha_wait": (c_int, [c_void_p, c_uint64]),
     "mirsha_poll": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),

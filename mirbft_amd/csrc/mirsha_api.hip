@@ -462,11 +462,14 @@ int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint
     HIP_TRY(c, p->d_cfirst.ensure(sizeof(uint32_t) * (n_lists + 1)));
     HIP_TRY(c, p->d_order.ensure(sizeof(uint32_t) * std::max<uint32_t>(n_req, 1)));
     HIP_TRY(c, p->d_state.ensure(32ull * std::max<uint32_t>(n_lists, 1)));
+    // Copies on the context stream (not the legacy null stream); the host
+    // vectors must outlive them, hence the synchronize.
     if (p->n_entries)
-        HIP_TRY(c, hipMemcpy(p->d_cidx.p, p->cidx.data(), sizeof(uint32_t) * p->n_entries, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(p->d_cfirst.p, p->cfirst.data(), sizeof(uint32_t) * (n_lists + 1), hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemcpyAsync(p->d_cidx.p, p->cidx.data(), sizeof(uint32_t) * p->n_entries, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(p->d_cfirst.p, p->cfirst.data(), sizeof(uint32_t) * (n_lists + 1), hipMemcpyHostToDevice, c->stream));
     if (n_req)
-        HIP_TRY(c, hipMemcpy(p->d_order.p, p->order.data(), sizeof(uint32_t) * n_req, hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemcpyAsync(p->d_order.p, p->order.data(), sizeof(uint32_t) * n_req, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     p->chunk_done.resize(S, nullptr);
     for (auto& e : p->chunk_done)
         if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -619,7 +622,10 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     // Device copies.
     auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
         HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
-        if (bytes) HIP_TRY(c, hipMemcpy(d.p, h, bytes, hipMemcpyHostToDevice));
+        if (bytes) {
+            HIP_TRY(c, hipMemcpyAsync(d.p, h, bytes, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(c, hipStreamSynchronize(c->stream));
+        }
         return MIRSHA_OK;
     };
     if (int rc = up(p->d_cidx, p->cidx.data(), sizeof(uint32_t) * p->n_entries)) return rc;
@@ -630,9 +636,11 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     if (int rc = up(p->d_cbase, p->cbase.data(), sizeof(uint32_t) * (p->n_groups + 1))) return rc;
     if (int rc = up(p->d_expected, p->expected.data(), sizeof(uint32_t) * p->expected.size())) return rc;
     HIP_TRY(c, p->d_counters.ensure(8ull * std::max<uint32_t>(p->n_counters, 1)));
-    HIP_TRY(c, hipMemset(p->d_counters.p, 0, 8ull * std::max<uint32_t>(p->n_counters, 1)));
+    HIP_TRY(c, hipMemsetAsync(p->d_counters.p, 0, 8ull * std::max<uint32_t>(p->n_counters, 1), c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, p->d_ctl.ensure(8ull * mirsha::kCtlWords));
-    HIP_TRY(c, hipMemset(p->d_ctl.p, 0, 8ull * mirsha::kCtlWords));
+    HIP_TRY(c, hipMemsetAsync(p->d_ctl.p, 0, 8ull * mirsha::kCtlWords, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     p->tile_base = p->list_base = 0;
     p->epoch = 0;
     const char* tr = getenv("MIRSHA_FUSED_TRACE");
@@ -640,7 +648,8 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     if (p->trace) {
         const size_t words = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
         HIP_TRY(c, p->d_trace.ensure(8ull * std::max<size_t>(words, 1)));
-        HIP_TRY(c, hipMemset(p->d_trace.p, 0, 8ull * std::max<size_t>(words, 1)));
+        HIP_TRY(c, hipMemsetAsync(p->d_trace.p, 0, 8ull * std::max<size_t>(words, 1), c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
     return MIRSHA_OK;
 }
@@ -689,7 +698,8 @@ int fused_status(mirsha_ctx* c, mirsha_pipeline* p) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (p->mode != MIRSHA_PIPELINE_FUSED || !p->d_ctl.p) return MIRSHA_OK;
     unsigned long long e = 0;
-    HIP_TRY(c, hipMemcpy(&e, p->d_ctl.as<unsigned long long>() + mirsha::kCtlError, 8, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpyAsync(&e, p->d_ctl.as<unsigned long long>() + mirsha::kCtlError, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (e) return fail(c, MIRSHA_EHIP, "fused pass: a list wave's readiness wait expired (watchdog)");
     return MIRSHA_OK;
 }
@@ -957,7 +967,7 @@ int mirsha_ctx_set_stream(mirsha_ctx* c, void* s) {
 void* mirsha_ctx_stream(mirsha_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
 
 int mirsha_ctx_set_variant(mirsha_ctx* c, int v) {
-    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantPair) return MIRSHA_EINVAL;
+    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantLdsOld) return MIRSHA_EINVAL;
     c->variant = v;
     return MIRSHA_OK;
 }
@@ -1056,6 +1066,18 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
     HIP_TRY(c, hipMemcpyAsync(out, c->d_out.p, 32ull * n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return MIRSHA_OK;
+}
+
+int mirsha_host_alloc(mirsha_ctx* c, uint64_t bytes, void** out) {
+    if (!c || !out) return MIRSHA_EINVAL;
+    *out = nullptr;
+    if (int rc = use_device(c)) return rc;
+    HIP_TRY(c, hipHostMalloc(out, std::max<uint64_t>(bytes, 1), hipHostMallocDefault));
+    return MIRSHA_OK;
+}
+
+void mirsha_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int mirsha_hash_slices_dedup(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
@@ -1215,7 +1237,10 @@ int mirsha_pipeline_trace(mirsha_ctx* c, mirsha_pipeline* p, uint64_t* out, uint
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const uint64_t n = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
     *words = n;
-    if (out && cap) HIP_TRY(c, hipMemcpy(out, p->d_trace.p, 8ull * std::min(n, cap), hipMemcpyDeviceToHost));
+    if (out && cap) {
+        HIP_TRY(c, hipMemcpyAsync(out, p->d_trace.p, 8ull * std::min(n, cap), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
     return MIRSHA_OK;
 }
 
@@ -1343,9 +1368,10 @@ int mirsha_chains_create(mirsha_ctx* c, uint32_t n, mirsha_chains** out) {
         HIP_TRY(c, ch->d_h.ensure(32ull * n));
         HIP_TRY(c, ch->d_pend.ensure(32ull * n));
         HIP_TRY(c, ch->d_cnt.ensure(8ull * n));
-        HIP_TRY(c, hipMemcpy(ch->d_h.p, h.data(), 32ull * n, hipMemcpyHostToDevice));
-        HIP_TRY(c, hipMemset(ch->d_pend.p, 0, 32ull * n));
-        HIP_TRY(c, hipMemset(ch->d_cnt.p, 0, 8ull * n));
+        HIP_TRY(c, hipMemcpyAsync(ch->d_h.p, h.data(), 32ull * n, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipMemsetAsync(ch->d_pend.p, 0, 32ull * n, c->stream));
+        HIP_TRY(c, hipMemsetAsync(ch->d_cnt.p, 0, 8ull * n, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
         return MIRSHA_OK;
     };
     if (int rc = up()) {

@@ -21,7 +21,9 @@ enum : int {
     kVariantDirectCxx = 3,
     kVariantLowOcc = 4,
     kVariantLdsOnly = 5,
-    kVariantPair = 6
+    kVariantPair = 6,
+    kVariantLdsPf = 7,  // LDS loader, next block's loads in flight during the rounds
+    kVariantLdsOld = 8  // round-1 LDS loader (per-chunk activity and range tests)
 };
 constexpr uint32_t kLowOccTiles = 1024;   // 256 CUs x 4 SIMDs
 // Small launches take a latency form: at most pair_max_groups() 64-message

@@ -24,6 +24,15 @@
 
 namespace mirsha {
 
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+        uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64);
+        v = v < o ? v : o;
+    }
+    return v;
+}
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
     for (int s = 1; s < 64; s <<= 1) {
@@ -161,7 +170,10 @@ __device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uin
 // One wave hashes the tile of 64 messages at processing positions
 // [64 t, 64 t + 64) (order[] maps a position to a message; NULL = identity).
 // kSc1Out: digests are stored through `ors` with the sc1 policy (fused pass).
-template <bool kLds, bool kAsm, bool kSc1Out, bool kWide = false>
+// kPf (LDS loader only): block b+1's raw chunks are issued right after block
+// b's words leave LDS, so their loads are in flight during b's compression
+// (+20 VGPRs live across the rounds).
+template <bool kLds, bool kAsm, bool kSc1Out, bool kWide = false, bool kPf = false, bool kOld = false>
 __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
@@ -193,6 +205,73 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     if constexpr (kLds) {
         // Loader roles: this lane fetches quarter q of messages m_j = 16j + lane/4.
         const uint32_t q = lane & 3u;
+        if constexpr (!kWide && !kPf && !kOld) {
+            // Chunk addresses are loop-invariant VGPRs with the block in the
+            // scalar offset.  There is no per-chunk activity test: a finished
+            // message's chunk reads bytes nobody uses (in range) or zeros (out
+            // of range).  A tile whose every load stays in the arena (all but
+            // the arena's last tiles; a wave-uniform test) takes plain
+            // loads; the others range-check each active-size chunk (the
+            // 5-dword tail form of issue_chunk).  The FIPS padding logic runs
+            // only on blocks that reach past the wave's shortest message.
+            const uint64_t reach = valid ? o + 64ull * wave_nb + 20u : 0ull;
+            const bool far = __builtin_amdgcn_ballot_w64(reach > records) == 0;
+            const uint32_t min_l = wave_min(valid ? L : 0xFFFFFFFFu);
+            uint32_t vo[4], sel[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t a = (uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) + 16u * q;
+                vo[j] = a & ~3u;
+                sel[j] = be_sel(a & 3u);
+            }
+            for (uint32_t blk = 0; blk < wave_nb; blk++) {
+                const uint32_t soff = 64u * blk;
+                RawChunk rc[4];
+                if (far) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], soff, 0);
+                        rc[j].v[0] = v[0]; rc[j].v[1] = v[1]; rc[j].v[2] = v[2]; rc[j].v[3] = v[3];
+                        rc[j].v[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo[j], soff + 16u, 0);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) issue_chunk(rsrc, (uint32_t)records, vo[j] + soff, 0u, 0u, true, rc[j]);
+                }
+                const bool pad = soff + 64u > min_l;  // wave-uniform
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    uint32_t wq[4];
+                    rc[j].sel = sel[j];
+                    if (pad) {
+                        // Lengths fetched here (rare blocks), not kept live
+                        // across the rounds.
+                        const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(lane >> 2), 64);
+                        finish_chunk(rc[j], soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; k++) wq[k] = be_word(rc[j].v[k + 1], rc[j].v[k], rc[j].sel);
+                    }
+                    // Unconditional: a slot of a finished message is never read.
+                    my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+                }
+                // Cross-lane hand-off inside one wave: LDS ops of a wave execute
+                // in order; the fences only stop the compiler from reordering.
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+                    w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (blk < nb) compress_v<kAsm>(st, w);
+            }
+        } else {
         uint32_t Lj[4], nbj[4];
         uint64_t oj[4];
 #pragma unroll
@@ -203,10 +282,16 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             if constexpr (kWide) oj[j] |= (uint64_t)(uint32_t)__shfl((int)(uint32_t)(o >> 32), src, 64) << 32;
             nbj[j] = (uint32_t)__shfl((int)nb, src, 64);
         }
-        for (uint32_t blk = 0; blk < wave_nb; blk++) {
-            RawChunk rc[4];
+        RawChunk rc[4];
+        if constexpr (kPf) {
 #pragma unroll
-            for (int j = 0; j < 4; j++) issue(oj[j], blk, q, blk < nbj[j], rc[j]);
+            for (int j = 0; j < 4; j++) issue(oj[j], 0u, q, 0u < nbj[j], rc[j]);
+        }
+        for (uint32_t blk = 0; blk < wave_nb; blk++) {
+            if constexpr (!kPf) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) issue(oj[j], blk, q, blk < nbj[j], rc[j]);
+            }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 uint32_t wq[4];
@@ -228,7 +313,14 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if constexpr (kPf) {
+                if (blk + 1u < wave_nb) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) issue(oj[j], blk + 1u, q, blk + 1u < nbj[j], rc[j]);
+                }
+            }
             if (blk < nb) compress_v<kAsm>(st, w);
+        }
         }
     } else {
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
@@ -251,7 +343,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     }
 }
 
-template <bool kLds, bool kAsm, bool kWide = false>
+template <bool kLds, bool kAsm, bool kWide = false, bool kPf = false, bool kOld = false>
 __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
@@ -261,7 +353,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * kWavesPerBlock + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<kLds, kAsm, false, kWide>(arena, arena_len, off, len, order, n, out,
+    hash_tile<kLds, kAsm, false, kWide, kPf, kOld>(arena, arena_len, off, len, order, n, out,
                                  __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000), tile[wv], t,
                                  lane);
 }
@@ -1068,10 +1160,27 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
+    // MIRSHA_MSGS_OCC=k (A/B): cap the waves per SIMD at k by reserving LDS
+    // (each 4-wave workgroup takes 1/k of the CU's 160 KiB).
+    static const size_t occ_lds = [] {
+        const char* e = getenv("MIRSHA_MSGS_OCC");
+        const uint32_t k = e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+        const size_t stat = sizeof(uint4) * kWavesPerBlock * 256u;
+        return (k >= 1 && k <= 8) ? (size_t)(160u * 1024u / k) - stat : (size_t)0;
+    }();
     switch (variant) {
         case kVariantLds:
         case kVariantLdsOnly:
-            sha256_msgs_kernel<true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+            sha256_msgs_kernel<true, true><<<grid, kBlockThreads, occ_lds, s>>>(arena, arena_len, off, len, order, n,
+                                                                               out);
+            break;
+        case kVariantLdsPf:
+            sha256_msgs_kernel<true, true, false, true><<<grid, kBlockThreads, occ_lds, s>>>(arena, arena_len, off, len,
+                                                                                          order, n, out);
+            break;
+        case kVariantLdsOld:
+            sha256_msgs_kernel<true, true, false, false, true><<<grid, kBlockThreads, occ_lds, s>>>(
+                arena, arena_len, off, len, order, n, out);
             break;
         case kVariantDirect:
             sha256_msgs_kernel<false, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);

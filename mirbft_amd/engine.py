@@ -35,6 +35,8 @@ VARIANT_DIRECT_CXX = 3
 VARIANT_LOWOCC = 4
 VARIANT_LDS_ONLY = 5
 VARIANT_PAIR = 6
+VARIANT_LDS_PF = 7
+VARIANT_LDS_OLD = 8
 
 
 def _ptr(a: np.ndarray | None) -> int | None:
@@ -96,6 +98,16 @@ class Ticket:
     def __init__(self, value: int, out: np.ndarray):
         self.value = value
         self.out = out
+
+
+def _out_rows(out, n: int) -> np.ndarray:
+    """A caller-supplied (n, 32) uint8 result array (checked), or a new one."""
+    if out is None:
+        return np.empty((n, 32), dtype=np.uint8)
+    if not isinstance(out, np.ndarray) or out.dtype != np.uint8 or out.shape != (n, 32) or not out.flags.c_contiguous \
+            or not out.flags.writeable:
+        raise ValueError(f"out must be a writeable C-contiguous uint8 array of shape ({n}, 32)")
+    return out
 
 
 def dedup_plan(requests) -> tuple[np.ndarray, int]:
@@ -176,15 +188,16 @@ class Engine:
         self._check(self._lib.mirsha_sync(self.ctx))
 
     # ------------------------------------------------------------ host API
-    def hash_batch(self, arena, off: Sequence[int], length: Sequence[int]) -> np.ndarray:
-        """Digest of arena[off[i]:off[i]+len[i]] for every i (processor.go:133-143)."""
+    def hash_batch(self, arena, off: Sequence[int], length: Sequence[int], out=None) -> np.ndarray:
+        """Digest of arena[off[i]:off[i]+len[i]] for every i (processor.go:133-143).
+        out: optional reusable uint8 (n, 32) result array."""
         a = _as_u8(arena)
         o = np.ascontiguousarray(off, dtype=np.uint64)
         ln = np.ascontiguousarray(length, dtype=np.uint32)
         if o.shape != ln.shape:
             raise ValueError("off and len differ in length")
         n = int(o.size)
-        out = np.empty((n, 32), dtype=np.uint8)
+        out = _out_rows(out, n)
         if n:
             self._check(self._lib.mirsha_hash_batch(self.ctx, _ptr(a), a.size, _ptr(o), _ptr(ln), n, _ptr(out)))
         return out
@@ -222,6 +235,18 @@ class Engine:
             self.last_unique = n
         return out
 
+    def host_empty(self, nbytes: int) -> np.ndarray:
+        """A uint8 array in page-locked host memory (mirsha_host_alloc), freed
+        with the array: the caller's arena at PCIe rate."""
+        p = ctypes.c_void_p()
+        self._check(self._lib.mirsha_host_alloc(self.ctx, int(nbytes), ctypes.byref(p)))
+        buf = (ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value)
+        arr = np.frombuffer(buf, dtype=np.uint8, count=int(nbytes))
+        import weakref
+
+        weakref.finalize(buf, self._lib.mirsha_host_free, p.value)
+        return arr
+
     def submit_slices(self, requests, dedup: bool = False) -> "Ticket":
         """Asynchronous, order-preserving submission (mirsha_submit_slices): the
         requests are packed before this returns; ``wait(ticket)`` yields the
@@ -243,8 +268,13 @@ class Engine:
         self._check(self._lib.mirsha_poll(self.ctx, ticket.value, ctypes.byref(done)))
         return bool(done.value)
 
-    def hash_requests_then_batches(self, arena, off, length, idx, batch_first):
-        """Request digests, then batch digests over them on device (sequence.go:154-157)."""
+    def hash_requests_then_batches(self, arena, off, length, idx, batch_first, out=None, batch_out=None):
+        """Request digests, then batch digests over them on device (sequence.go:154-157).
+
+        out / batch_out: optional C-contiguous uint8 (n, 32) / (n_batches, 32)
+        arrays reused across calls.  A fresh 32 MiB result array costs ~30 ms
+        of first-touch page faults per call (glibc hands large allocations
+        out as new mmaps), which is more than the GPU work at 1M requests."""
         a = _as_u8(arena)
         o = np.ascontiguousarray(off, dtype=np.uint64)
         ln = np.ascontiguousarray(length, dtype=np.uint32)
@@ -253,8 +283,8 @@ class Engine:
         n, nb = int(o.size), int(fs.size) - 1
         if nb < 0:
             raise ValueError("batch_first needs n_batches + 1 entries")
-        req = np.empty((n, 32), dtype=np.uint8)
-        bat = np.empty((nb, 32), dtype=np.uint8)
+        req = _out_rows(out, n)
+        bat = _out_rows(batch_out, nb)
         self._check(
             self._lib.mirsha_hash_requests_then_batches(
                 self.ctx, _ptr(a), a.size, _ptr(o), _ptr(ln), n, _ptr(ix), _ptr(fs), nb, _ptr(req), _ptr(bat)
@@ -470,4 +500,6 @@ __all__ = [
     "VARIANT_LOWOCC",
     "VARIANT_LDS_ONLY",
     "VARIANT_PAIR",
+    "VARIANT_LDS_PF",
+    "VARIANT_LDS_OLD",
 ]

@@ -15,7 +15,8 @@ from mirbft_amd import (ActionResults, Actions, Engine, HashRequest, MirshaError
                         gpu_hasher, hash_batch_multi, hashdata, sharding)
 from mirbft_amd import _lib
 from mirbft_amd.engine import (KERNEL_LISTS, KERNEL_MSGS, VARIANT_DIRECT, VARIANT_DIRECT_CXX, VARIANT_LDS,
-                               VARIANT_LDS_CXX, VARIANT_LDS_ONLY, VARIANT_LOWOCC, VARIANT_PAIR)
+                               VARIANT_LDS_CXX, VARIANT_LDS_OLD, VARIANT_LDS_ONLY, VARIANT_LDS_PF, VARIANT_LOWOCC,
+                               VARIANT_PAIR)
 
 pytestmark = pytest.mark.gpu
 
@@ -23,8 +24,8 @@ EMPTY = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 
 
 @pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LDS_CXX, VARIANT_DIRECT_CXX, VARIANT_LOWOCC,
-                        VARIANT_LDS_ONLY, VARIANT_PAIR],
-                ids=["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only", "pair"])
+                        VARIANT_LDS_ONLY, VARIANT_PAIR, VARIANT_LDS_PF, VARIANT_LDS_OLD],
+                ids=["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only", "pair", "lds_pf", "lds_old"])
 def eng(engine, request):
     engine.set_variant(request.param)
     yield engine
@@ -195,6 +196,28 @@ def test_requests_then_batches_random_with_nulls(eng):
     want_req = oracle_py.hash_requests(arena, off, lens)
     assert np.array_equal(req, want_req)
     assert np.array_equal(bat, oracle_py.batch_digests(want_req, idx, first))
+
+
+def test_pinned_host_arena(engine, synth_fx):
+    """An arena in mirsha_host_alloc memory (the Go side's reused C arena)
+    gives the same digests as a pageable one."""
+    fx = synth_fx["cfg2_prefix"]
+    n, bs = fx["count"], fx["batch_size"]
+    src = synth.request_arena(synth.SEED_BASE + 2, 0, n, 256).reshape(-1)
+    arena = engine.host_empty(src.size)
+    arena[:] = src
+    idx, first = sharding.batch_lists(n, bs)
+    req_buf = np.zeros((n, 32), np.uint8)
+    bat_buf = np.zeros((len(first) - 1, 32), np.uint8)
+    for _ in range(2):  # result buffers reused across calls
+        req, bat = engine.hash_requests_then_batches(arena, np.arange(n) * 272, np.full(n, 272), idx, first,
+                                                     out=req_buf, batch_out=bat_buf)
+        assert req is req_buf and bat is bat_buf
+        assert hashlib.sha256(req.tobytes()).hexdigest() == fx["request_sha256_of_concat"]
+        assert _hex(bat) == fx["batch_sha256"]
+    assert engine.host_empty(0).size == 0
+    with pytest.raises(ValueError):
+        engine.hash_batch(arena, [0], [272], out=np.zeros((2, 32), np.uint8))
 
 
 def test_invalid_arguments_raise(engine):
