@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mirbft_amd import Engine, sharding  # noqa: E402
-from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
+from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_CONT, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
 
 SEED_BASE = 0x6D69726266740000
 # Algorithmic work unit: one 64-byte SHA-256 compression = 1384 int32 VALU ops
@@ -82,7 +82,7 @@ def parse():
     p.add_argument("--dedup", type=int, default=1, help="config 4: 1 = mirsha_hash_slices_dedup, 0 = plain")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-API measurement")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential", "streams"],
+    p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential", "streams", "cont"],
                    help="auto: mirsha_pipeline plan, AUTO mode (fused launch for long chains, else request "
                         "kernel then list kernel); none: plain device API (request kernel, then batch kernel); "
                         "fused / sequential / streams: force a plan mode (A/B)")
@@ -169,6 +169,11 @@ class BatchWorkload:
 
     def dominant(self):
         """(kernel name, launches, ms, compressions, algorithmic HBM bytes) of the dominant kernel."""
+        n_c, ms_c = self.eng.kernel_time(KERNEL_CONT)
+        if n_c:
+            # One launch: request tiles plus the batch segments they complete.
+            hbm = self.n * self.stride + self.n * 32 + self.n * 32 + self.nbat * 32
+            return "sha256_msgs_cont_kernel", n_c, ms_c, self.req_blocks + self.bat_blocks, hbm
         n_f, ms_f = self.eng.kernel_time(KERNEL_FUSED)
         if n_f:
             # One launch does the request AND the batch compressions.
@@ -265,6 +270,8 @@ class BatchWorkload:
         return {"batch_kernel_avg_ms": self.batch_ms() / self.a.steps,
                 "batch_pass": {"none": "sequential batch kernel (plain device API)",
                                "fused": "fused into the request launch (readiness counters, no second kernel)",
+                               "cont": "continuation: the request wave completing a batch segment hashes it "
+                                       "(one launch, no waits)",
                                "sequential": "plan: request kernel then batch kernel",
                                "streams": "chain segments on a second stream"}[mode]}
 

@@ -226,15 +226,24 @@ int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, uint32
  *   MIRSHA_PIPELINE_STREAMS: requests in needed-at chunks with batch-chain
  *     segments on a second stream (midstate carried on device); measured
  *     slower at BASELINE sizes, kept for A/B.
+ *   MIRSHA_PIPELINE_CONT: ONE launch at full occupancy for many short lists
+ *     that are contiguous request ranges (the batches of a cycle in origin
+ *     order; BatchSize a multiple of 4, >= 8).  Requests are hashed segment by
+ *     segment (ordinals [0,8), [8,16), [16,20) at BatchSize 20); the request
+ *     wave that completes a (64-list group, segment) counter hashes that
+ *     segment's blocks itself, so batch chains advance beside later request
+ *     tiles and only the last 2-3 blocks trail the launch.  Other shapes fall
+ *     back to SEQUENTIAL (mirsha_pipeline_mode() reports it).
  *   MIRSHA_PIPELINE_AUTO (default): FUSED when the longest list is >= 64
  *     blocks (~126 digests) and there are <= 64 list groups, else SEQUENTIAL;
  *     mirsha_pipeline_mode() reports the choice.
  * mirsha_pipeline_create reads MIRSHA_PIPELINE_MODE (auto | fused |
- * sequential | streams; default auto). */
+ * sequential | streams | cont; default auto). */
 #define MIRSHA_PIPELINE_SEQUENTIAL 0
 #define MIRSHA_PIPELINE_FUSED 1
 #define MIRSHA_PIPELINE_STREAMS 2
 #define MIRSHA_PIPELINE_AUTO 3
+#define MIRSHA_PIPELINE_CONT 4
 typedef struct mirsha_pipeline mirsha_pipeline;
 int mirsha_pipeline_create(mirsha_ctx* ctx, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
                            const uint32_t* list_first, uint32_t n_lists, mirsha_pipeline** out);

@@ -102,7 +102,7 @@ struct mirsha_ctx {
     std::string err;
     DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
     PinnedBuf h_stage;
-    KernelTimer timers[5];         // msgs, lists, gen, chain, fused
+    KernelTimer timers[6];         // msgs, lists, gen, chain, fused, cont
     hipStream_t chain_stream = nullptr;  // dependent-pass stream of the pipeline (lazy)
     AsyncSlot slots[kAsyncSlots];
     uint64_t next_ticket = 1;  // ticket of the next submission
@@ -138,6 +138,10 @@ struct mirsha_pipeline {
     std::vector<hipEvent_t> chunk_done;      // one per chain segment
     hipEvent_t chain_done = nullptr;
     DevBuf d_cidx, d_cfirst, d_order, d_state;
+    // continuation mode (sha256_msgs_cont_kernel)
+    std::vector<uint32_t> ctarget;
+    uint32_t cont_flags = 0;                 // mirsha::kContLatFinal (MIRSHA_CONT_FLAGS)
+    DevBuf d_ctarget, d_cplan;
 };
 
 namespace {
@@ -704,6 +708,170 @@ int fused_status(mirsha_ctx* c, mirsha_pipeline* p) {
     return MIRSHA_OK;
 }
 
+// ---- continuation plan: one request launch, list segments ride on it --------
+//
+// Admitted shape (else the plan falls back to SEQUENTIAL): contiguous lists
+// from request 0 with no null entries (list k = requests [first[k],
+// first[k+1]): the batches of one Ready() cycle in origin order,
+// sequence.go:154-157), every list B requests but the last (1..B), B a
+// multiple of 4 and >= 8, so that with segment bounds on multiples of 4 no
+// 128-byte line of request digests feeds two (group, segment) pairs.
+bool cont_shape(const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint32_t n_req, uint32_t* B) {
+    if (n_lists == 0 || first[0] != 0) return false;
+    const uint32_t b = first[1] - first[0];
+    if (b < 8 || b % 4u != 0 || first[n_lists] > n_req) return false;
+    for (uint32_t k = 0; k < n_lists; k++) {
+        const uint32_t c = first[k + 1] - first[k];
+        if (k + 1 < n_lists ? c != b : (c == 0 || c > b)) return false;
+    }
+    for (uint32_t e = 0; e < first[n_lists]; e++)
+        if (idx[e] != e) return false;
+    *B = b;
+    return true;
+}
+
+// Segment bounds (ordinals, multiples of 4): the last segment holds the last
+// 4 ordinals (2 digest blocks + the padding block trail the launch), the rest
+// is split in two.  MIRSHA_CONT_BOUNDS="8,16" overrides (A/B).
+std::vector<uint32_t> cont_bounds(uint32_t B) {
+    std::vector<uint32_t> b{0};
+    if (const char* e = getenv("MIRSHA_CONT_BOUNDS")) {
+        for (const char* s = e; *s;) {
+            char* end = nullptr;
+            const uint32_t v = (uint32_t)strtoul(s, &end, 10);
+            if (end == s) break;
+            if (v > b.back() && v < B && v % 4u == 0 && b.size() < mirsha::kContMaxSegments) b.push_back(v);
+            s = *end ? end + 1 : end;
+        }
+        return b;
+    }
+    const uint32_t last = B - 4u;
+    const uint32_t mid = (last / 2u) & ~3u;
+    if (mid > 0) b.push_back(mid);
+    if (last > b.back()) b.push_back(last);
+    return b;
+}
+
+int cont_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t* first, uint32_t n_lists, uint32_t B) {
+    p->n_req = n_req;
+    p->n_lists = n_lists;
+    p->n_entries = first[n_lists];
+    p->cfirst.assign(first, first + n_lists + 1);
+    p->seg_bound = cont_bounds(B);
+    const uint32_t S = (uint32_t)p->seg_bound.size();
+    auto seg_of = [&](uint32_t o) -> uint32_t {
+        return (uint32_t)(std::upper_bound(p->seg_bound.begin(), p->seg_bound.end(), o) - p->seg_bound.begin()) - 1u;
+    };
+    // Processing order: segment of the ordinal (unlisted requests last), then
+    // request index.
+    const uint32_t listed = first[n_lists];
+    std::vector<uint32_t> cnt(S + 2, 0);
+    for (uint32_t r = 0; r < n_req; r++) cnt[(r < listed ? seg_of(r % B) : S) + 1]++;
+    for (uint32_t s = 0; s <= S; s++) cnt[s + 1] += cnt[s];
+    const std::vector<uint32_t> seg_first(cnt.begin(), cnt.end());  // first position of each segment
+    p->order.assign(n_req, 0);
+    std::vector<uint32_t> pos_of(n_req);
+    for (uint32_t r = 0; r < n_req; r++) {
+        const uint32_t s = r < listed ? seg_of(r % B) : S;
+        pos_of[r] = cnt[s];
+        p->order[cnt[s]++] = r;
+    }
+    p->n_tiles = (n_req + 63u) / 64u;
+    p->n_groups = (n_lists + 63u) / 64u;
+    p->n_counters = p->n_groups * S;
+    std::vector<uint64_t> pairs;
+    pairs.reserve(listed / 8u + 1u);
+    for (uint32_t r = 0; r < listed; r++)
+        pairs.push_back(((uint64_t)(pos_of[r] >> 6) << 32) | ((r / B) / 64u * S + seg_of(r % B)));
+    std::sort(pairs.begin(), pairs.end());
+    pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
+    p->tadj_first.assign(p->n_tiles + 1, 0);
+    p->tadj.resize(pairs.size());
+    p->ctarget.assign(p->n_counters, 0);
+    for (size_t i = 0; i < pairs.size(); i++) {
+        p->tadj_first[(pairs[i] >> 32) + 1]++;
+        p->tadj[i] = (uint32_t)pairs[i];
+        p->ctarget[(uint32_t)pairs[i]]++;
+    }
+    for (uint32_t t = 0; t < p->n_tiles; t++) p->tadj_first[t + 1] += p->tadj_first[t];
+    for (uint32_t g = 0; g < p->n_groups; g++) {
+        if (p->ctarget[g * S] == 0) return fail(c, MIRSHA_EINVAL, "cont plan: group %u has no segment-0 tile", g);
+        for (uint32_t s = 1; s < S; s++) p->ctarget[g * S + s]++;  // + the previous segment's signal
+    }
+    p->cont_flags = 0;
+    if (const char* e = getenv("MIRSHA_CONT_FLAGS")) p->cont_flags = (uint32_t)atoi(e);
+    auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
+        HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
+        if (bytes) HIP_TRY(c, hipMemcpyAsync(d.p, h, bytes, hipMemcpyHostToDevice, c->stream));
+        return MIRSHA_OK;
+    };
+    if (int rc = up(p->d_cfirst, p->cfirst.data(), sizeof(uint32_t) * (n_lists + 1))) return rc;
+    if (int rc = up(p->d_order, p->order.data(), sizeof(uint32_t) * n_req)) return rc;
+    if (int rc = up(p->d_tadj_first, p->tadj_first.data(), sizeof(uint32_t) * (p->n_tiles + 1))) return rc;
+    if (int rc = up(p->d_tadj, p->tadj.data(), sizeof(uint32_t) * p->tadj.size())) return rc;
+    if (int rc = up(p->d_ctarget, p->ctarget.data(), sizeof(uint32_t) * p->ctarget.size())) return rc;
+    // Fallback of a misaligned output (cont_run): the chain kernel over the
+    // (identity) compacted lists.
+    p->cidx.resize(listed);
+    for (uint32_t e = 0; e < listed; e++) p->cidx[e] = e;
+    if (int rc = up(p->d_cidx, p->cidx.data(), sizeof(uint32_t) * listed)) return rc;
+    HIP_TRY(c, p->d_counters.ensure(8ull * std::max<uint32_t>(p->n_counters, 1)));
+    HIP_TRY(c, hipMemsetAsync(p->d_counters.p, 0, 8ull * std::max<uint32_t>(p->n_counters, 1), c->stream));
+    HIP_TRY(c, p->d_state.ensure(32ull * std::max<uint32_t>(S - 1u, 1u) * n_lists));
+    mirsha::ContPlan cp{};
+    cp.cfirst = p->d_cfirst.as<uint32_t>();
+    cp.tadj_first = p->d_tadj_first.as<uint32_t>();
+    cp.tadj = p->d_tadj.as<uint32_t>();
+    cp.ctarget = p->d_ctarget.as<uint32_t>();
+    cp.counters = p->d_counters.as<unsigned long long>();
+    cp.state = p->d_state.as<uint32_t>();
+    cp.n_lists = n_lists;
+    cp.n_seg = S;
+    cp.flags = p->cont_flags;
+    for (uint32_t s = 0; s < S; s++) {
+        cp.bound[s] = p->seg_bound[s];
+        cp.seg_tile[s] = seg_first[s] / 64u;
+    }
+    if (int rc = up(p->d_cplan, &cp, sizeof(cp))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors / cp outlive the copies
+    p->epoch = 0;
+    return MIRSHA_OK;
+}
+
+int cont_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
+             const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
+    if (p->n_req == 0) return MIRSHA_OK;
+    if ((reinterpret_cast<uintptr_t>(d_req_out) & 127u) != 0 || arena_len > mirsha::kMaxBufferArena) {
+        // The line-exclusivity argument needs 128-B aligned digests; the
+        // 32-bit loader needs the arena in one descriptor.  Two kernels.
+        if (int rc = timed_launch(c, 0, [&] {
+                return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, nullptr, p->n_req, d_req_out, c->variant,
+                                           c->stream);
+            }))
+            return rc;
+        return timed_launch(c, 1, [&] {
+            return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
+                                        p->d_cfirst.as<uint32_t>(), p->n_lists, 0u, mirsha::kOpenEnd,
+                                        p->d_state.as<uint32_t>(), d_list_out, c->stream);
+        });
+    }
+    mirsha::ContArgs a{};
+    a.arena = d_arena;
+    a.arena_len = arena_len;
+    a.off = d_off;
+    a.len = d_len;
+    a.order = p->d_order.as<uint32_t>();
+    a.req_out = d_req_out;
+    a.list_out = d_list_out;
+    a.plan = p->d_cplan.as<mirsha::ContPlan>();
+    a.n_req = p->n_req;
+    a.epoch = p->epoch + 1u;
+    a.flags = p->cont_flags;
+    if (int rc = timed_launch(c, 5, [&] { return mirsha::launch_cont(a, c->stream); })) return rc;
+    p->epoch++;
+    return MIRSHA_OK;
+}
+
 // AUTO: the fused launch pays when a few LONG chains would otherwise run after
 // the request pass (VerifyBatch of hundreds of digests, BASELINE config 3:
 // 1.49 -> 1.04 ms); many short lists (BatchSize 20, config 2) run better as
@@ -723,6 +891,11 @@ int plan_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t
                uint32_t n_lists, const uint32_t* len) {
     if (p->mode == MIRSHA_PIPELINE_AUTO)
         p->mode = fused_pays(idx, first, n_lists) ? MIRSHA_PIPELINE_FUSED : MIRSHA_PIPELINE_SEQUENTIAL;
+    if (p->mode == MIRSHA_PIPELINE_CONT) {
+        uint32_t B = 0;
+        if (cont_shape(idx, first, n_lists, n_req, &B)) return cont_build(c, p, n_req, first, n_lists, B);
+        p->mode = MIRSHA_PIPELINE_SEQUENTIAL;  // shape not admitted: two kernels
+    }
     if (p->mode == MIRSHA_PIPELINE_FUSED) return fused_build(c, p, n_req, idx, first, n_lists, len);
     return pipeline_build(c, p, n_req, idx, first, n_lists, len);
 }
@@ -730,6 +903,7 @@ int plan_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t
 int plan_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
              const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
     if (p->mode == MIRSHA_PIPELINE_FUSED) return fused_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
+    if (p->mode == MIRSHA_PIPELINE_CONT) return cont_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
     return pipeline_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
 }
 
@@ -738,6 +912,7 @@ int default_pipeline_mode() {
     if (m && strcmp(m, "sequential") == 0) return MIRSHA_PIPELINE_SEQUENTIAL;
     if (m && strcmp(m, "streams") == 0) return MIRSHA_PIPELINE_STREAMS;
     if (m && strcmp(m, "fused") == 0) return MIRSHA_PIPELINE_FUSED;
+    if (m && strcmp(m, "cont") == 0) return MIRSHA_PIPELINE_CONT;
     return MIRSHA_PIPELINE_AUTO;
 }
 
@@ -756,6 +931,8 @@ void pipeline_free(mirsha_pipeline* p) {
     p->d_counters.release();
     p->d_ctl.release();
     p->d_trace.release();
+    p->d_ctarget.release();
+    p->d_cplan.release();
 }
 
 
@@ -979,7 +1156,7 @@ int mirsha_ctx_set_timing(mirsha_ctx* c, int enable) {
 }
 
 int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double* total_ms) {
-    if (!c || which < 0 || which > 4) return MIRSHA_EINVAL;
+    if (!c || which < 0 || which > 5) return MIRSHA_EINVAL;
     if (int rc = use_device(c)) return rc;
     KernelTimer& t = c->timers[which];
     for (auto& pr : t.pending) {
@@ -999,7 +1176,7 @@ int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double*
 
 int mirsha_ctx_reset_timing(mirsha_ctx* c) {
     if (!c) return MIRSHA_EINVAL;
-    for (int k = 0; k < 5; k++) {
+    for (int k = 0; k < 6; k++) {
         int rc = mirsha_ctx_kernel_time(c, k, nullptr, nullptr);
         if (rc) return rc;
         c->timers[k].launches = 0;
@@ -1152,7 +1329,7 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
     // device API (mirsha_pipeline_create + *_device) amortises one plan.
     const char* pmode = getenv("MIRSHA_PIPELINE_MODE");
     const bool pipelined = pmode && (strcmp(pmode, "fused") == 0 || strcmp(pmode, "streams") == 0 ||
-                                     strcmp(pmode, "auto") == 0);
+                                     strcmp(pmode, "auto") == 0 || strcmp(pmode, "cont") == 0);
     if (pipelined && n_batches && n_req && span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES &&
         span <= 2 * total + 4096) {
         mirsha_pipeline p;
@@ -1204,7 +1381,7 @@ int mirsha_pipeline_create_mode(mirsha_ctx* c, uint32_t n_req, const uint32_t* l
                                 const uint32_t* list_first, uint32_t n_lists, int mode, mirsha_pipeline** out) {
     if (!c || !out) return MIRSHA_EINVAL;
     *out = nullptr;
-    if (mode < MIRSHA_PIPELINE_SEQUENTIAL || mode > MIRSHA_PIPELINE_AUTO) return fail(c, MIRSHA_EINVAL, "bad mode %d", mode);
+    if (mode < MIRSHA_PIPELINE_SEQUENTIAL || mode > MIRSHA_PIPELINE_CONT) return fail(c, MIRSHA_EINVAL, "bad mode %d", mode);
     if (int rc = check_lists(c, idx, list_first, n_lists, n_req)) return rc;
     if (int rc = use_device(c)) return rc;
     mirsha_pipeline* p = new mirsha_pipeline();

@@ -90,6 +90,44 @@ constexpr uint32_t kFusedTileYield = 2;  // issue-yield rounds in tile waves (pa
 // (kPacedLds of reserved LDS), `pace` tile waves per SIMD in tile blocks.
 constexpr uint32_t kPacedLds = 96u * 1024u;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
+// Continuation plan (MIRSHA_PIPELINE_CONT), see mirsha_kernels.hip: the
+// request launch at full occupancy; the tile wave that completes a list
+// group's segment counter hashes that segment itself (no waiting anywhere).
+// Lists are contiguous request ranges (list k = requests [cfirst[k],
+// cfirst[k+1])), segments cover ordinals [bound[s], bound[s+1]).
+constexpr uint32_t kContMaxSegments = 4;
+// Plan constants, in device memory (read only after a tile's own work, so
+// none of it stays live in registers across the request rounds).
+struct ContPlan {
+    const uint32_t* cfirst;      // n_lists + 1
+    const uint32_t* tadj_first;  // n_tiles + 1: counters each tile feeds
+    const uint32_t* tadj;
+    const uint32_t* ctarget;     // per counter (g * n_seg + s): feeding tiles + (s > 0)
+    unsigned long long* counters;
+    uint32_t* state;             // (n_seg - 1) x n_lists midstates, sc1 stores/loads
+    uint32_t n_lists, n_seg, flags, pad;
+    uint32_t bound[kContMaxSegments];
+    uint32_t seg_tile[kContMaxSegments];  // first tile of each segment's requests (processing order)
+};
+struct ContArgs {
+    const uint8_t* arena;
+    uint64_t arena_len;
+    const uint64_t* off;
+    const uint32_t* len;
+    const uint32_t* order;       // n_req processing positions -> request
+    uint8_t* req_out;            // n_req digests, origin order (sc1 stores)
+    uint8_t* list_out;
+    const ContPlan* plan;        // device copy
+    uint32_t n_req, epoch, flags;  // flags: the plan's (kContSkipLists / kContPlainStores read here)
+};
+// MIRSHA_CONT_FLAGS (A/B knobs)
+constexpr uint32_t kContLatFinal = 1;  // no-yield rounds in final segments
+constexpr uint32_t kContNoPrio = 2;    // no issue priorities (default: segments 3, tiles 2 - their segment)
+constexpr uint32_t kContSkipLists = 4;  // timing only: request tiles alone (list digests NOT computed)
+constexpr uint32_t kContPlainStores = 8;  // timing only: plain digest stores (no cross-CU visibility)
+constexpr uint32_t kContNoSegments = 16;  // timing only: counter adds, but no segment is hashed
+constexpr uint32_t kContLatAll = 32;     // no-yield rounds in every segment
+hipError_t launch_cont(const ContArgs& a, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.
 hipError_t launch_chains_absorb(const uint8_t* digests, const uint32_t* pos, const uint32_t* act, const uint32_t* afirst,

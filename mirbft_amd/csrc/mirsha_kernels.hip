@@ -1064,6 +1064,173 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     }
 }
 
+// ---- continuation plan: request launch + list segments, no waits -----------
+//
+// Many short lists (BatchSize 20, BASELINE config 2): a separate list launch
+// runs 820 lone chain waves of 11 compressions after the request kernel (37 us
+// of a 247 us step).  Here the request kernel keeps its full occupancy and
+// the list work rides on it: requests are processed in segment order (all
+// ordinals of segment 0 of every list first, then segment 1, ...), every tile
+// adds 1 to the counter of each (list group, segment) it feeds after its sc1
+// digest stores drained, and the wave whose add COMPLETES a counter hashes
+// that segment of the group's 64 lists (lane = list) at once, then adds 1 to
+// the next segment's counter (which also waits for its own tiles); whoever
+// completes that one continues.  Nobody waits, so there is no deadlock and
+// no watchdog.  Segments of early groups interleave with later request tiles
+// at full occupancy; only the last segments (<= 2 digest blocks + padding)
+// trail the launch.
+//
+// Visibility: digests and midstates are stored sc1 (written through, dropped
+// from the writer's L2) and read sc1 by the completing wave after the
+// counter said every producer's stores drained.  The plan admits a shape only
+// if no 128-B line of request digests is shared by two (group, segment)
+// pairs (contiguous lists, BatchSize and segment bounds multiples of 4,
+// 128-B aligned output), so no L2 can hold a line before it is complete.
+// Midstates: one region per segment, each line written once and read once per
+// run.
+template <bool kLat>
+__device__ __forceinline__ void cont_segment(const ContPlan& a, uint8_t* list_out, __amdgpu_buffer_rsrc_t drs,
+                                             __amdgpu_buffer_rsrc_t srs, uint32_t g, uint32_t s, uint32_t lane) {
+    const uint32_t k = g * 64u + lane;
+    const bool valid = k < a.n_lists;
+    const uint32_t e0 = valid ? a.cfirst[k] : 0u;  // first request of the list (contiguous lists)
+    const uint32_t c = valid ? a.cfirst[k + 1] - e0 : 0u;
+    const uint32_t ob = a.bound[s];
+    const uint32_t oe = s + 1u < a.n_seg ? a.bound[s + 1u] : kOpenEnd;
+    const bool active = valid && (ob == 0u || c > ob);
+    const bool fin = active && c <= oe;
+    const uint32_t full_end = fin ? (c & ~1u) : oe;  // exclusive ordinal of the full blocks
+    const uint32_t nblk = active ? (full_end - ob) / 2u + (fin ? 1u : 0u) : 0u;
+    const uint32_t wave_nb = wave_max(nblk);
+    const uint32_t L = 32u * c;
+    uint32_t st[8];
+    if (ob == 0u) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    } else {
+        const uint32_t so = 32u * ((s - 1u) * a.n_lists + k);
+        const auto x0 = __builtin_amdgcn_raw_buffer_load_b128(srs, active ? so : 0xFFFFFFE0u, 0, kSc1);
+        const auto x1 = __builtin_amdgcn_raw_buffer_load_b128(srs, active ? so + 16u : 0xFFFFFFE0u, 0, kSc1);
+        st[0] = x0[0]; st[1] = x0[1]; st[2] = x0[2]; st[3] = x0[3];
+        st[4] = x1[0]; st[5] = x1[1]; st[6] = x1[2]; st[7] = x1[3];
+    }
+    for (uint32_t t = 0; t < wave_nb; t++) {
+        const uint32_t d0 = ob + 2u * t;
+        uint4 x[4];
+        load_digest_sc1(drs, e0 + d0, t < nblk && d0 < c, x[0], x[1]);
+        load_digest_sc1(drs, e0 + d0 + 1u, t < nblk && d0 + 1u < c, x[2], x[3]);
+        uint32_t w[16];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const uint32_t di = d0 + (uint32_t)half;
+            const uint4 x0 = x[2 * half], x1 = x[2 * half + 1];
+            // Past the end the loads returned zeros; only the 0x80 marker is added.
+            w[8 * half + 0] = __builtin_bswap32(x0.x) | (fin && di == c ? 0x80000000u : 0u);
+            w[8 * half + 1] = __builtin_bswap32(x0.y); w[8 * half + 2] = __builtin_bswap32(x0.z);
+            w[8 * half + 3] = __builtin_bswap32(x0.w); w[8 * half + 4] = __builtin_bswap32(x1.x);
+            w[8 * half + 5] = __builtin_bswap32(x1.y); w[8 * half + 6] = __builtin_bswap32(x1.z);
+            w[8 * half + 7] = __builtin_bswap32(x1.w);
+        }
+        if (fin && t + 1u == nblk) {
+            w[14] = L >> 29;
+            w[15] = L << 3;
+        }
+        if (t < nblk) {
+            if constexpr (kLat)
+                compress_asm_lat(st, w);
+            else
+                compress_asm(st, w);
+        }
+    }
+    if (fin) {
+        store_digest(list_out, k, st);
+    } else if (active) {
+        const uint32_t so = 32u * (s * a.n_lists + k);
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){st[0], st[1], st[2], st[3]}, srs, so, 0, kSc1);
+        __builtin_amdgcn_raw_buffer_store_b128((v4u){st[4], st[5], st[6], st[7]}, srs, so + 16u, 0, kSc1);
+    }
+}
+
+// Runs segment `ctr` (wave-uniform counter id, just completed) and every later
+// segment of the same group whose counter this wave then completes.
+__device__ __forceinline__ void cont_chain(const ContPlan& a, uint8_t* list_out, uint32_t epoch, __amdgpu_buffer_rsrc_t drs,
+                                          __amdgpu_buffer_rsrc_t srs, uint32_t ctr, uint32_t lane) {
+    while (true) {
+        const uint32_t g = ctr / a.n_seg, s = ctr - g * a.n_seg;
+        const bool last = s + 1u == a.n_seg;
+        asm volatile("" ::: "memory");  // no load of the segment above the completing add
+        if ((last && (a.flags & kContLatFinal)) || (a.flags & kContLatAll))
+            cont_segment<true>(a, list_out, drs, srs, g, s, lane);
+        else
+            cont_segment<false>(a, list_out, drs, srs, g, s, lane);
+        if (last) return;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // midstate stores drained before the signal
+        uint32_t go = 0;
+        if (lane == 0) {
+            const unsigned long long old =
+                __hip_atomic_fetch_add(a.counters + ctr + 1u, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            go = old + 1ull == (unsigned long long)epoch * a.ctarget[ctr + 1u];
+        }
+        if (!__shfl((int)go, 0, 64)) return;
+        ctr++;
+    }
+}
+
+// One wave per workgroup: a wave that goes on to hash list segments must not
+// hold a finished workgroup's LDS and slots (4-wave workgroups: 0.397 ms per
+// config-2 launch, 1-wave: 0.332 ms).  Issue priorities: segments 3 (they are the
+// critical path to the launch's end), tiles 2 - the segment they feed, so the
+// tiles that feed later segments yield to those that complete earlier ones.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sha256_msgs_cont_kernel(ContArgs ca) {
+    __shared__ uint4 tile[256];
+    const uint32_t t = blockIdx.x;
+    if (t * 64u >= ca.n_req) return;
+    {
+        const ContPlan& p = *ca.plan;
+        if (!(p.flags & kContNoPrio)) {
+            const uint32_t ph = (p.n_seg > 1u && t >= p.seg_tile[1]) + (p.n_seg > 2u && t >= p.seg_tile[2]);
+            if (ph == 0)
+                __builtin_amdgcn_s_setprio(2);
+            else if (ph == 1)
+                __builtin_amdgcn_s_setprio(1);
+        }
+    }
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)ca.req_out, (short)0, (int)(32u * ca.n_req), 0x00020000);
+    if (ca.flags & kContPlainStores)
+        hash_tile<true, true, false>(ca.arena, ca.arena_len, ca.off, ca.len, ca.order, ca.n_req, ca.req_out, drs, tile,
+                                     t, threadIdx.x & 63u);
+    else
+        hash_tile<true, true, true>(ca.arena, ca.arena_len, ca.off, ca.len, ca.order, ca.n_req, nullptr, drs, tile, t,
+                                    threadIdx.x & 63u);
+    if (ca.flags & kContSkipLists) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's digest stores drained before its adds
+    // Recomputed rather than kept live across the rounds (VGPR budget of 8 waves per SIMD).
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const ContPlan& p = *ca.plan;
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.state, (short)0, (int)(32u * (p.n_seg - 1u) * p.n_lists), 0x00020000);
+    const uint32_t j0 = p.tadj_first[t], j1 = p.tadj_first[t + 1];
+    for (uint32_t j = j0; j < j1; j += 64u) {
+        const bool mine = j + lane < j1;
+        const uint32_t ctr = mine ? p.tadj[j + lane] : 0u;
+        bool done = false;
+        if (mine) {
+            const unsigned long long old =
+                __hip_atomic_fetch_add(p.counters + ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            done = old + 1ull == (unsigned long long)ca.epoch * p.ctarget[ctr] && !(ca.flags & kContNoSegments);
+        }
+        uint64_t m = __builtin_amdgcn_ballot_w64(done);
+        if (m && !(p.flags & kContNoPrio)) __builtin_amdgcn_s_setprio(3);
+        while (m) {
+            const int l = __builtin_ctzll(m);
+            m &= m - 1u;
+            cont_chain(p, ca.list_out, ca.epoch, drs, srs, (uint32_t)__shfl((int)ctr, l, 64), lane);
+        }
+    }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1233,6 +1400,13 @@ hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, 
         attr = true;
     }
     sha256_fused_paced_kernel<<<grid, 256u * pace, kPacedLds, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cont(const ContArgs& a, hipStream_t s) {
+    if (a.n_req == 0) return hipSuccess;
+    if (!a.plan || a.arena_len > kMaxBufferArena) return hipErrorInvalidValue;
+    sha256_msgs_cont_kernel<<<(a.n_req + 63u) / 64u, 64, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -20,14 +20,16 @@ KERNEL_LISTS = 1
 KERNEL_GEN = 2
 KERNEL_CHAIN = 3
 KERNEL_FUSED = 4
+KERNEL_CONT = 5
 
 # mirsha_pipeline modes (include/mirsha.h)
 PIPELINE_SEQUENTIAL = 0
 PIPELINE_FUSED = 1
 PIPELINE_STREAMS = 2
 PIPELINE_AUTO = 3
+PIPELINE_CONT = 4
 PIPELINE_MODES = {"sequential": PIPELINE_SEQUENTIAL, "fused": PIPELINE_FUSED, "streams": PIPELINE_STREAMS,
-                  "auto": PIPELINE_AUTO}
+                  "auto": PIPELINE_AUTO, "cont": PIPELINE_CONT}
 VARIANT_LDS = 0
 VARIANT_DIRECT = 1
 VARIANT_LDS_CXX = 2
@@ -491,6 +493,7 @@ __all__ = [
     "KERNEL_GEN",
     "KERNEL_CHAIN",
     "KERNEL_FUSED",
+    "KERNEL_CONT",
     "PIPELINE_SEQUENTIAL",
     "PIPELINE_FUSED",
     "PIPELINE_STREAMS",
