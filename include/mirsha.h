@@ -89,8 +89,12 @@ int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 /* Per-kernel device-time accounting with HIP events on the launch stream.
  * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator,
  * 3 = pipelined batch-chain segments (on the context's second stream),
- * 4 = fused request -> batch kernel (one persistent launch per run). */
+ * 4 = fused request -> batch kernel (one persistent launch per run),
+ * 5 = continuation request -> batch kernel (MIRSHA_PIPELINE_CONT).
+ * set_timing_mask: bit k on = kernel k is timed while timing is enabled
+ * (default: all); each timed launch adds two event records to its stream. */
 int mirsha_ctx_set_timing(mirsha_ctx* ctx, int enable);
+int mirsha_ctx_set_timing_mask(mirsha_ctx* ctx, uint32_t mask);
 int mirsha_ctx_kernel_time(mirsha_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
 int mirsha_ctx_reset_timing(mirsha_ctx* ctx);
 

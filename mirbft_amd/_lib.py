@@ -45,6 +45,7 @@ SIGNATURES = {
     "mirsha_ctx_stream": (c_void_p, [c_void_p]),
     "mirsha_ctx_set_variant": (c_int, [c_void_p, c_int]),
     "mirsha_ctx_set_timing": (c_int, [c_void_p, c_int]),
+    "mirsha_ctx_set_timing_mask": (c_int, [c_void_p, c_uint32]),
     "mirsha_ctx_kernel_time": (c_int, [c_void_p, c_int, _u64p, POINTER(c_double)]),
     "mirsha_ctx_reset_timing": (c_int, [c_void_p]),
     "mirsha_sync": (c_int, [c_void_p]),

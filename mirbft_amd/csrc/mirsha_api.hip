@@ -99,6 +99,7 @@ struct mirsha_ctx {
     hipStream_t stream = nullptr;
     int variant = mirsha::kVariantLds;
     bool timing = false;
+    uint32_t time_mask = 0xFFFFFFFFu;  // kernels timed while timing is on
     std::string err;
     DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
     PinnedBuf h_stage;
@@ -179,14 +180,15 @@ hipEvent_t take_event(KernelTimer& t) {
 template <class F>
 int timed_launch_on(mirsha_ctx* c, int which, hipStream_t st, F&& launch) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->timing) {
+    const bool timed = c->timing && ((c->time_mask >> which) & 1u);
+    if (timed) {
         e0 = take_event(c->timers[which]);
         e1 = take_event(c->timers[which]);
         if (e0) (void)hipEventRecord(e0, st);
     }
     hipError_t e = launch();
     if (e != hipSuccess) return fail(c, MIRSHA_EHIP, "kernel launch: %s", hipGetErrorString(e));
-    if (c->timing && e0 && e1) {
+    if (timed && e0 && e1) {
         (void)hipEventRecord(e1, st);
         c->timers[which].pending.emplace_back(e0, e1);
     }
@@ -1171,6 +1173,12 @@ int mirsha_ctx_kernel_time(mirsha_ctx* c, int which, uint64_t* launches, double*
     t.pending.clear();
     if (launches) *launches = t.launches;
     if (total_ms) *total_ms = t.ms;
+    return MIRSHA_OK;
+}
+
+int mirsha_ctx_set_timing_mask(mirsha_ctx* c, uint32_t mask) {
+    if (!c) return MIRSHA_EINVAL;
+    c->time_mask = mask;
     return MIRSHA_OK;
 }
 

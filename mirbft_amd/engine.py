@@ -183,6 +183,13 @@ class Engine:
         self._check(self._lib.mirsha_ctx_kernel_time(self.ctx, int(kernel), ctypes.byref(n), ctypes.byref(ms)))
         return n.value, ms.value
 
+    def set_timing_mask(self, kernels) -> None:
+        """Time only these kernel ids (KERNEL_*) while timing is enabled."""
+        m = 0
+        for k in kernels:
+            m |= 1 << int(k)
+        self._check(self._lib.mirsha_ctx_set_timing_mask(self.ctx, m))
+
     def reset_timing(self) -> None:
         self._check(self._lib.mirsha_ctx_reset_timing(self.ctx))
 
