@@ -108,10 +108,7 @@ __device__ __forceinline__ void issue_chunk_wide(const uint8_t* __restrict__ are
 // Big-endian SHA words of the chunk at message byte position p, with FIPS
 // 180-4 §5.1.1 padding (0x80, zeros, 64-bit bit length in words 14/15 of the
 // last block) applied branch-free on chunks that reach past the message end.
-__device__ __forceinline__ void finish_chunk(const RawChunk& c, uint32_t p, uint32_t L, bool last_block,
-                                             uint32_t q, uint32_t out[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) out[k] = be_word(c.v[k + 1], c.v[k], c.sel);
+__device__ __forceinline__ void pad_words(uint32_t p, uint32_t L, bool last_block, uint32_t q, uint32_t out[4]) {
     if (p + 16u > L) {
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -127,6 +124,13 @@ __device__ __forceinline__ void finish_chunk(const RawChunk& c, uint32_t p, uint
             out[3] = L << 3;
         }
     }
+}
+
+__device__ __forceinline__ void finish_chunk(const RawChunk& c, uint32_t p, uint32_t L, bool last_block,
+                                             uint32_t q, uint32_t out[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) out[k] = be_word(c.v[k + 1], c.v[k], c.sel);
+    pad_words(p, L, last_block, q, out);
 }
 
 // Swizzled 16-byte slot of (message m, quarter q) inside a wave's 256-slot tile.
@@ -216,7 +220,10 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             // only on blocks that reach past the wave's shortest message.
             const uint64_t reach = valid ? o + 64ull * wave_nb + 20u : 0ull;
             const bool far = __builtin_amdgcn_ballot_w64(reach > records) == 0;
-            const uint32_t min_l = wave_min(valid ? L : 0xFFFFFFFFu);
+            // Wave-uniform by construction; readfirstlane makes it an SGPR, so
+            // the padding test below is a scalar branch (as a VGPR compare it
+            // became an exec-mask branch with the word assembly duplicated).
+            const uint32_t min_l = __builtin_amdgcn_readfirstlane(wave_min(valid ? L : 0xFFFFFFFFu));
             uint32_t vo[4], sel[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -242,15 +249,13 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     uint32_t wq[4];
-                    rc[j].sel = sel[j];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) wq[k] = be_word(rc[j].v[k + 1], rc[j].v[k], sel[j]);
                     if (pad) {
                         // Lengths fetched here (rare blocks), not kept live
                         // across the rounds.
                         const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(lane >> 2), 64);
-                        finish_chunk(rc[j], soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 4; k++) wq[k] = be_word(rc[j].v[k + 1], rc[j].v[k], rc[j].sel);
+                        pad_words(soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
                     }
                     // Unconditional: a slot of a finished message is never read.
                     my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
