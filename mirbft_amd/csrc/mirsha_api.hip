@@ -830,6 +830,15 @@ int cont_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t
     cp.n_lists = n_lists;
     cp.n_seg = S;
     cp.flags = p->cont_flags;
+    cp.n_tiles = p->n_tiles;
+    const char* tr = getenv("MIRSHA_CONT_TRACE");
+    p->trace = tr && atoi(tr) != 0;
+    if (p->trace) {
+        const size_t words = 2ull * p->n_tiles + 2ull * p->n_counters;
+        HIP_TRY(c, p->d_trace.ensure(8ull * words));
+        HIP_TRY(c, hipMemsetAsync(p->d_trace.p, 0, 8ull * words, c->stream));
+        cp.trace = p->d_trace.as<unsigned long long>();
+    }
     for (uint32_t s = 0; s < S; s++) {
         cp.bound[s] = p->seg_bound[s];
         cp.seg_tile[s] = seg_first[s] / 64u;
@@ -1417,10 +1426,11 @@ int mirsha_pipeline_mode(const mirsha_pipeline* p) { return p ? p->mode : MIRSHA
 int mirsha_pipeline_trace(mirsha_ctx* c, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words) {
     if (!c || !p || !words) return MIRSHA_EINVAL;
     *words = 0;
-    if (p->mode != MIRSHA_PIPELINE_FUSED || !p->trace) return MIRSHA_OK;
+    if ((p->mode != MIRSHA_PIPELINE_FUSED && p->mode != MIRSHA_PIPELINE_CONT) || !p->trace) return MIRSHA_OK;
     if (int rc = use_device(c)) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    const uint64_t n = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
+    const uint64_t n = p->mode == MIRSHA_PIPELINE_CONT ? 2ull * p->n_tiles + 2ull * p->n_counters
+                                                        : 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
     *words = n;
     if (out && cap) {
         HIP_TRY(c, hipMemcpyAsync(out, p->d_trace.p, 8ull * std::min(n, cap), hipMemcpyDeviceToHost, c->stream));

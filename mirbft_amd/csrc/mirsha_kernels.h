@@ -105,9 +105,13 @@ struct ContPlan {
     const uint32_t* ctarget;     // per counter (g * n_seg + s): feeding tiles + (s > 0)
     unsigned long long* counters;
     uint32_t* state;             // (n_seg - 1) x n_lists midstates, sc1 stores/loads
-    uint32_t n_lists, n_seg, flags, pad;
+    uint32_t n_lists, n_seg, flags, n_tiles;
     uint32_t bound[kContMaxSegments];
     uint32_t seg_tile[kContMaxSegments];  // first tile of each segment's requests (processing order)
+    // Optional timeline (s_memrealtime, 100 MHz), NULL = off: per tile [start,
+    // end] at [2t, 2t+1], per counter c = g * n_seg + s its segment's [start,
+    // end] at [2 n_tiles + 2c, +1].
+    unsigned long long* trace;
 };
 struct ContArgs {
     const uint8_t* arena;

@@ -1165,10 +1165,15 @@ __device__ __forceinline__ void cont_chain(const ContPlan& a, uint8_t* list_out,
         const uint32_t g = ctr / a.n_seg, s = ctr - g * a.n_seg;
         const bool last = s + 1u == a.n_seg;
         asm volatile("" ::: "memory");  // no load of the segment above the completing add
+        if (a.trace && lane == 0) a.trace[2ull * a.n_tiles + 2ull * ctr] = __builtin_amdgcn_s_memrealtime();
         if ((last && (a.flags & kContLatFinal)) || (a.flags & kContLatAll))
             cont_segment<true>(a, list_out, drs, srs, g, s, lane);
         else
             cont_segment<false>(a, list_out, drs, srs, g, s, lane);
+        if (a.trace) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) a.trace[2ull * a.n_tiles + 2ull * ctr + 1u] = __builtin_amdgcn_s_memrealtime();
+        }
         if (last) return;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // midstate stores drained before the signal
         uint32_t go = 0;
@@ -1203,6 +1208,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     }
     const __amdgpu_buffer_rsrc_t drs =
         __builtin_amdgcn_make_buffer_rsrc((void*)ca.req_out, (short)0, (int)(32u * ca.n_req), 0x00020000);
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     if (ca.flags & kContPlainStores)
         hash_tile<true, true, false>(ca.arena, ca.arena_len, ca.off, ca.len, ca.order, ca.n_req, ca.req_out, drs, tile,
                                      t, threadIdx.x & 63u);
@@ -1214,6 +1220,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     // Recomputed rather than kept live across the rounds (VGPR budget of 8 waves per SIMD).
     const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     const ContPlan& p = *ca.plan;
+    if (p.trace && (threadIdx.x & 63u) == 0) {
+        p.trace[2ull * t] = t_start;
+        p.trace[2ull * t + 1u] = __builtin_amdgcn_s_memrealtime();
+    }
     const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
         (void*)p.state, (short)0, (int)(32u * (p.n_seg - 1u) * p.n_lists), 0x00020000);
     const uint32_t j0 = p.tadj_first[t], j1 = p.tadj_first[t + 1];
