@@ -1114,16 +1114,18 @@ __device__ __forceinline__ void cont_segment(const ContPlan& a, uint8_t* list_ou
         for (int i = 0; i < 8; i++) st[i] = kH0[i];
     } else {
         const uint32_t so = 32u * ((s - 1u) * a.n_lists + k);
-        const auto x0 = __builtin_amdgcn_raw_buffer_load_b128(srs, active ? so : 0xFFFFFFE0u, 0, kSc1);
-        const auto x1 = __builtin_amdgcn_raw_buffer_load_b128(srs, active ? so + 16u : 0xFFFFFFE0u, 0, kSc1);
+        const bool ld = active && !(a.flags & kContSegNoLoads);
+        const auto x0 = __builtin_amdgcn_raw_buffer_load_b128(srs, ld ? so : 0xFFFFFFE0u, 0, kSc1);
+        const auto x1 = __builtin_amdgcn_raw_buffer_load_b128(srs, ld ? so + 16u : 0xFFFFFFE0u, 0, kSc1);
         st[0] = x0[0]; st[1] = x0[1]; st[2] = x0[2]; st[3] = x0[3];
         st[4] = x1[0]; st[5] = x1[1]; st[6] = x1[2]; st[7] = x1[3];
     }
     for (uint32_t t = 0; t < wave_nb; t++) {
         const uint32_t d0 = ob + 2u * t;
         uint4 x[4];
-        load_digest_sc1(drs, e0 + d0, t < nblk && d0 < c, x[0], x[1]);
-        load_digest_sc1(drs, e0 + d0 + 1u, t < nblk && d0 + 1u < c, x[2], x[3]);
+        const bool ld = !(a.flags & kContSegNoLoads);
+        load_digest_sc1(drs, e0 + d0, ld && t < nblk && d0 < c, x[0], x[1]);
+        load_digest_sc1(drs, e0 + d0 + 1u, ld && t < nblk && d0 + 1u < c, x[2], x[3]);
         uint32_t w[16];
 #pragma unroll
         for (int half = 0; half < 2; half++) {
@@ -1140,11 +1142,14 @@ __device__ __forceinline__ void cont_segment(const ContPlan& a, uint8_t* list_ou
             w[14] = L >> 29;
             w[15] = L << 3;
         }
-        if (t < nblk) {
+        if (t < nblk && !(a.flags & kContSegNoCompress)) {
             if constexpr (kLat)
                 compress_asm_lat(st, w);
             else
                 compress_asm(st, w);
+        } else if (t < nblk) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) st[i] ^= w[i] ^ w[i + 8];  // keep the loads live
         }
     }
     if (fin) {
