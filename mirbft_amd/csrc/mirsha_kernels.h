@@ -133,6 +133,7 @@ constexpr uint32_t kContNoSegments = 16;  // timing only: counter adds, but no s
 constexpr uint32_t kContLatAll = 32;     // no-yield rounds in every segment
 constexpr uint32_t kContSegNoLoads = 64;     // timing only: segments read no digests / state (wrong digests)
 constexpr uint32_t kContSegNoCompress = 128; // timing only: segments load but do not compress (wrong digests)
+constexpr uint32_t kContSegLowPrio = 256;    // tiles priority 1, segments 0 (segments fill issue bubbles)
 hipError_t launch_cont(const ContArgs& a, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.

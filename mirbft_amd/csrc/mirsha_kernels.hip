@@ -1203,7 +1203,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
     if (t * 64u >= ca.n_req) return;
     {
         const ContPlan& p = *ca.plan;
-        if (!(p.flags & kContNoPrio)) {
+        if (p.flags & kContSegLowPrio) {
+            __builtin_amdgcn_s_setprio(1);
+        } else if (!(p.flags & kContNoPrio)) {
             const uint32_t ph = (p.n_seg > 1u && t >= p.seg_tile[1]) + (p.n_seg > 2u && t >= p.seg_tile[2]);
             if (ph == 0)
                 __builtin_amdgcn_s_setprio(2);
@@ -1242,7 +1244,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void
             done = old + 1ull == (unsigned long long)ca.epoch * p.ctarget[ctr] && !(ca.flags & kContNoSegments);
         }
         uint64_t m = __builtin_amdgcn_ballot_w64(done);
-        if (m && !(p.flags & kContNoPrio)) __builtin_amdgcn_s_setprio(3);
+        if (m && (p.flags & kContSegLowPrio))
+            __builtin_amdgcn_s_setprio(0);
+        else if (m && !(p.flags & kContNoPrio))
+            __builtin_amdgcn_s_setprio(3);
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1u;
