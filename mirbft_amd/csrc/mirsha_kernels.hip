@@ -1192,12 +1192,15 @@ __device__ __forceinline__ void cont_chain(const ContPlan& a, uint8_t* list_out,
     }
 }
 
+// Register budget left to hipcc (78 VGPRs, 6 waves per SIMD, no scratch):
+// forcing 8 waves per SIMD spilled 11 VGPRs to scratch and measured slower
+// with segments (0.346 vs 0.333 ms), equal without them (0.211 vs 0.210 ms).
 // One wave per workgroup: a wave that goes on to hash list segments must not
 // hold a finished workgroup's LDS and slots (4-wave workgroups: 0.397 ms per
 // config-2 launch, 1-wave: 0.332 ms).  Issue priorities: segments 3 (they are the
 // critical path to the launch's end), tiles 2 - the segment they feed, so the
 // tiles that feed later segments yield to those that complete earlier ones.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8, 8))) void sha256_msgs_cont_kernel(ContArgs ca) {
+__global__ __launch_bounds__(64) void sha256_msgs_cont_kernel(ContArgs ca) {
     __shared__ uint4 tile[256];
     const uint32_t t = blockIdx.x;
     if (t * 64u >= ca.n_req) return;
