@@ -126,14 +126,14 @@ struct ContArgs {
 };
 // MIRSHA_CONT_FLAGS (A/B knobs)
 constexpr uint32_t kContLatFinal = 1;  // no-yield rounds in final segments
-constexpr uint32_t kContNoPrio = 2;    // no issue priorities (default: segments 3, tiles 2 - their segment)
+constexpr uint32_t kContNoPrio = 2;    // no issue priorities (default: tiles 1, segments 0)
 constexpr uint32_t kContSkipLists = 4;  // timing only: request tiles alone (list digests NOT computed)
 constexpr uint32_t kContPlainStores = 8;  // timing only: plain digest stores (no cross-CU visibility)
 constexpr uint32_t kContNoSegments = 16;  // timing only: counter adds, but no segment is hashed
 constexpr uint32_t kContLatAll = 32;     // no-yield rounds in every segment
 constexpr uint32_t kContSegNoLoads = 64;     // timing only: segments read no digests / state (wrong digests)
 constexpr uint32_t kContSegNoCompress = 128; // timing only: segments load but do not compress (wrong digests)
-constexpr uint32_t kContSegLowPrio = 256;    // tiles priority 1, segments 0 (segments fill issue bubbles)
+constexpr uint32_t kContSegHighPrio = 256;   // segments 3, tiles 2 - the segment they feed (first design)
 hipError_t launch_cont(const ContArgs& a, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.

@@ -1197,18 +1197,18 @@ __device__ __forceinline__ void cont_chain(const ContPlan& a, uint8_t* list_out,
 // with segments (0.346 vs 0.333 ms), equal without them (0.211 vs 0.210 ms).
 // One wave per workgroup: a wave that goes on to hash list segments must not
 // hold a finished workgroup's LDS and slots (4-wave workgroups: 0.397 ms per
-// config-2 launch, 1-wave: 0.332 ms).  Issue priorities: segments 3 (they are the
-// critical path to the launch's end), tiles 2 - the segment they feed, so the
-// tiles that feed later segments yield to those that complete earlier ones.
+// config-2 launch, 1-wave: 0.332 ms).  Issue priorities: tiles 1, segments 0,
+// so a segment wave only fills the tiles' issue bubbles (0.277 ms; segments at
+// 3 and tiles by the segment they feed, the first design: 0.333 ms).
 __global__ __launch_bounds__(64) void sha256_msgs_cont_kernel(ContArgs ca) {
     __shared__ uint4 tile[256];
     const uint32_t t = blockIdx.x;
     if (t * 64u >= ca.n_req) return;
     {
         const ContPlan& p = *ca.plan;
-        if (p.flags & kContSegLowPrio) {
+        if (!(p.flags & (kContSegHighPrio | kContNoPrio))) {
             __builtin_amdgcn_s_setprio(1);
-        } else if (!(p.flags & kContNoPrio)) {
+        } else if (p.flags & kContSegHighPrio) {
             const uint32_t ph = (p.n_seg > 1u && t >= p.seg_tile[1]) + (p.n_seg > 2u && t >= p.seg_tile[2]);
             if (ph == 0)
                 __builtin_amdgcn_s_setprio(2);
@@ -1247,9 +1247,9 @@ __global__ __launch_bounds__(64) void sha256_msgs_cont_kernel(ContArgs ca) {
             done = old + 1ull == (unsigned long long)ca.epoch * p.ctarget[ctr] && !(ca.flags & kContNoSegments);
         }
         uint64_t m = __builtin_amdgcn_ballot_w64(done);
-        if (m && (p.flags & kContSegLowPrio))
+        if (m && !(p.flags & (kContSegHighPrio | kContNoPrio)))
             __builtin_amdgcn_s_setprio(0);
-        else if (m && !(p.flags & kContNoPrio))
+        else if (m && (p.flags & kContSegHighPrio))
             __builtin_amdgcn_s_setprio(3);
         while (m) {
             const int l = __builtin_ctzll(m);
