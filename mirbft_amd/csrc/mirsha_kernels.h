@@ -134,6 +134,8 @@ constexpr uint32_t kContLatAll = 32;     // no-yield rounds in every segment
 constexpr uint32_t kContSegNoLoads = 64;     // timing only: segments read no digests / state (wrong digests)
 constexpr uint32_t kContSegNoCompress = 128; // timing only: segments load but do not compress (wrong digests)
 constexpr uint32_t kContSegHighPrio = 256;   // segments 3, tiles 2 - the segment they feed (first design)
+constexpr uint32_t kContSegPrioTile = 512;   // segments at the tiles' priority (1)
+constexpr uint32_t kContSegPrioIndex = 1024; // segment s at priority min(s, 3)
 hipError_t launch_cont(const ContArgs& a, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.

@@ -1170,6 +1170,18 @@ __device__ __forceinline__ void cont_chain(const ContPlan& a, uint8_t* list_out,
         const uint32_t g = ctr / a.n_seg, s = ctr - g * a.n_seg;
         const bool last = s + 1u == a.n_seg;
         asm volatile("" ::: "memory");  // no load of the segment above the completing add
+        if (a.flags & kContSegPrioTile) {
+            __builtin_amdgcn_s_setprio(1);
+        } else if (a.flags & kContSegPrioIndex) {
+            if (s == 0)
+                __builtin_amdgcn_s_setprio(0);
+            else if (s == 1)
+                __builtin_amdgcn_s_setprio(1);
+            else if (s == 2)
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(3);
+        }
         if (a.trace && lane == 0) a.trace[2ull * a.n_tiles + 2ull * ctr] = __builtin_amdgcn_s_memrealtime();
         if ((last && (a.flags & kContLatFinal)) || (a.flags & kContLatAll))
             cont_segment<true>(a, list_out, drs, srs, g, s, lane);
