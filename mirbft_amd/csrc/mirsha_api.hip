@@ -831,6 +831,11 @@ int cont_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t
     cp.n_seg = S;
     cp.flags = p->cont_flags;
     cp.n_tiles = p->n_tiles;
+    {
+        double frac = 0.3;
+        if (const char* e = getenv("MIRSHA_CONT_PRIO_FRAC")) frac = atof(e);
+        cp.prio_tile = (uint32_t)(frac * p->n_tiles);
+    }
     const char* tr = getenv("MIRSHA_CONT_TRACE");
     p->trace = tr && atoi(tr) != 0;
     if (p->trace) {

@@ -108,6 +108,7 @@ struct ContPlan {
     uint32_t n_lists, n_seg, flags, n_tiles;
     uint32_t bound[kContMaxSegments];
     uint32_t seg_tile[kContMaxSegments];  // first tile of each segment's requests (processing order)
+    uint32_t prio_tile;                   // kContSegPrioLate threshold (MIRSHA_CONT_PRIO_FRAC x n_tiles)
     // Optional timeline (s_memrealtime, 100 MHz), NULL = off: per tile [start,
     // end] at [2t, 2t+1], per counter c = g * n_seg + s its segment's [start,
     // end] at [2 n_tiles + 2c, +1].
@@ -136,6 +137,7 @@ constexpr uint32_t kContSegNoCompress = 128; // timing only: segments load but d
 constexpr uint32_t kContSegHighPrio = 256;   // segments 3, tiles 2 - the segment they feed (first design)
 constexpr uint32_t kContSegPrioTile = 512;   // segments at the tiles' priority (1)
 constexpr uint32_t kContSegPrioIndex = 1024; // segment s at priority min(s, 3)
+constexpr uint32_t kContSegPrioLate = 2048;  // segments run by tiles t >= prio_tile at priority 2, others 0
 hipError_t launch_cont(const ContArgs& a, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.

@@ -1165,7 +1165,13 @@ __device__ __forceinline__ void cont_segment(const ContPlan& a, uint8_t* list_ou
 // Runs segment `ctr` (wave-uniform counter id, just completed) and every later
 // segment of the same group whose counter this wave then completes.
 __device__ __forceinline__ void cont_chain(const ContPlan& a, uint8_t* list_out, uint32_t epoch, __amdgpu_buffer_rsrc_t drs,
-                                          __amdgpu_buffer_rsrc_t srs, uint32_t ctr, uint32_t lane) {
+                                          __amdgpu_buffer_rsrc_t srs, uint32_t ctr, uint32_t lane, uint32_t t) {
+    if (a.flags & kContSegPrioLate) {
+        if (t >= a.prio_tile)
+            __builtin_amdgcn_s_setprio(2);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    }
     while (true) {
         const uint32_t g = ctr / a.n_seg, s = ctr - g * a.n_seg;
         const bool last = s + 1u == a.n_seg;
@@ -1266,7 +1272,7 @@ __global__ __launch_bounds__(64) void sha256_msgs_cont_kernel(ContArgs ca) {
         while (m) {
             const int l = __builtin_ctzll(m);
             m &= m - 1u;
-            cont_chain(p, ca.list_out, ca.epoch, drs, srs, (uint32_t)__shfl((int)ctr, l, 64), lane);
+            cont_chain(p, ca.list_out, ca.epoch, drs, srs, (uint32_t)__shfl((int)ctr, l, 64), lane, t);
         }
     }
 }
