@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mirbft_amd import Engine, sharding  # noqa: E402
-from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_CONT, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
+from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
 
 SEED_BASE = 0x6D69726266740000
 # Algorithmic work unit: one 64-byte SHA-256 compression = 1384 int32 VALU ops
@@ -73,19 +73,26 @@ def parse():
                    help="untimed steps; MI355X needs ~20+ ms of sustained load to reach its working clock")
     p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
-    p.add_argument("--variant", type=int, default=0, help="0 = LDS-staged loader (low-occupancy kernel for <= 1 wave/SIMD launches), "
-                        "1 = direct per-lane loads, 2/3 = C++ rounds, 4 = low-occupancy kernel, 5 = LDS kernel only, "
-                        "6 = pair kernel, 7 = LDS loader with one-block prefetch, 8 = round-1 LDS loader")
+    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6],
+                   help="0 = LDS-staged loader (latency forms for small launches), 1 = direct per-lane loads, "
+                        "4 = low-occupancy kernel, 5 = LDS kernel only, 6 = pair kernel")
     p.add_argument("--windows", action="store_true",
                    help="config 5: hash in <= 4 GiB windows (one launch each) instead of one 64-bit-addressed launch")
+    p.add_argument("--prewarm-ms", type=float, default=400.0,
+                   help="after the warm-up steps, keep running untimed steps until this much wall time has passed: "
+                        "the clock needs tens of ms of sustained load to settle, and the driver's --warmup 5 is "
+                        "~1.5 ms (reported as prewarm_ms / prewarm_steps)")
+    p.add_argument("--probe-iters", type=int, default=128,
+                   help="clock probe after the timed region (compressions per wave; 0 disables)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU baseline sample (0 disables)")
     p.add_argument("--dedup", type=int, default=1, help="config 4: 1 = mirsha_hash_slices_dedup, 0 = plain")
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-API measurement")
-    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential", "streams", "cont"],
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="PMC traffic per launch, keyed by kernel_source_key(); written by profiles/profile.sh")
+    p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential"],
                    help="auto: mirsha_pipeline plan, AUTO mode (fused launch for long chains, else request "
                         "kernel then list kernel); none: plain device API (request kernel, then batch kernel); "
-                        "fused / sequential / streams: force a plan mode (A/B)")
+                        "fused / sequential: force a plan mode (A/B)")
     p.add_argument("--timed-kernels", default="dominant", choices=["dominant", "all"],
                    help="kernels with HIP events inside the timed loop: the dominant (roofline) kernel only, "
                         "or every kernel (each timed launch adds two event records to the stream); with "
@@ -111,6 +118,58 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def _cpu_facts():
+    """What the CPU baseline ran on: the reference's ProcessorWorkPool default is
+    HashWorkers = runtime.NumCPU() (processor.go:406-408), and Go's NumCPU is the
+    size of the process's CPU affinity mask."""
+    facts = {"os_cpu_count": os.cpu_count()}
+    try:
+        facts["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        facts["affinity_cpus"] = os.cpu_count()
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        facts["cgroup_cpu_quota"] = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        facts["cgroup_cpu_quota"] = None
+    try:
+        facts["sha_ni"] = bool(_oracle().has_shani())
+    except Exception:  # noqa: BLE001 - informational only
+        facts["sha_ni"] = None
+    return facts
+
+
+def pool_threads():
+    """HashWorkers = runtime.NumCPU() (processor.go:406-408): the affinity mask."""
+    return _cpu_facts()["affinity_cpus"] or 1
+
+
+def kernel_source_key(variant):
+    """Identity of the kernel build whose PMC traffic a profile recorded: the
+    sha256 of the device sources plus the variant (the .so is not in git, the
+    sources are)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("mirsha_kernels.hip", "mirsha_kernels.h", "sha256_device.h", "sha256_rounds_asm.h"):
+        with open(os.path.join(ROOT, "mirbft_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    h.update(str(int(variant)).encode())
+    return h.hexdigest()[:16]
+
+
+def lookup_traffic(path, key, config):
+    """hbm_bytes_per_launch of the dominant kernel for this build, or None."""
+    try:
+        tf = json.load(open(path))
+    except (OSError, ValueError):
+        return None, None
+    for e in tf.get("entries", []):
+        if e.get("key") == key and int(e.get("config", -1)) == int(config):
+            return e.get("hbm_bytes_per_launch"), e
+    return None, None
 
 
 def _time_cpu(fn, seconds, threads_list):
@@ -173,11 +232,6 @@ class BatchWorkload:
 
     def dominant(self):
         """(kernel name, launches, ms, compressions, algorithmic HBM bytes) of the dominant kernel."""
-        n_c, ms_c = self.eng.kernel_time(KERNEL_CONT)
-        if n_c:
-            # One launch: request tiles plus the batch segments they complete.
-            hbm = self.n * self.stride + self.n * 32 + self.n * 32 + self.nbat * 32
-            return "sha256_msgs_cont_kernel", n_c, ms_c, self.req_blocks + self.bat_blocks, hbm
         n_f, ms_f = self.eng.kernel_time(KERNEL_FUSED)
         if n_f:
             # One launch does the request AND the batch compressions.
@@ -248,7 +302,7 @@ class BatchWorkload:
             d = o.hash_requests(arena, off, ln, threads=threads)
             o.batch_digests(d, idx, first)
 
-        res = _time_cpu(one, seconds, (1, min(16, os.cpu_count() or 1)))
+        res = _time_cpu(one, seconds, (1, pool_threads()))
         per = n + first.size - 1
         done1, dt1 = res[1]
         tp = max(res)
@@ -258,8 +312,10 @@ class BatchWorkload:
                       f"digests), {dt1:.1f} s, oracle C port of processor.go:133-143 (serial Processor), "
                       f"SHA-NI compression (stand-in for Go crypto/sha256 amd64 asm)",
             "pool": {"value": res[tp][0] * per / res[tp][1], "threads": tp,
-                     "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361)"},
+                     "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361), "
+                             "HashWorkers = runtime.NumCPU() = the affinity mask (processor.go:406-408)"},
             "cpu": _cpu_model(),
+            **_cpu_facts(),
         }
 
     def config_fields(self):
@@ -274,10 +330,7 @@ class BatchWorkload:
         return {"batch_kernel_avg_ms": self.batch_ms() / self.a.steps,
                 "batch_pass": {"none": "sequential batch kernel (plain device API)",
                                "fused": "fused into the request launch (readiness counters, no second kernel)",
-                               "cont": "continuation: the request wave completing a batch segment hashes it "
-                                       "(one launch, no waits)",
-                               "sequential": "plan: request kernel then batch kernel",
-                               "streams": "chain segments on a second stream"}[mode]}
+                               "sequential": "plan: request kernel then batch kernel"}[mode]}
 
 
 class MixedWorkload:
@@ -354,8 +407,7 @@ class MixedWorkload:
         o = _oracle()
         k = min(self.n, 30000)  # ~300 MB sample of the same stream
         arena, off, ln = o.gen_mixed(self.seed, np.arange(k, dtype=np.uint64))
-        res = _time_cpu(lambda t: o.hash_requests(arena, off, ln, threads=t), seconds,
-                        (1, min(16, os.cpu_count() or 1)))
+        res = _time_cpu(lambda t: o.hash_requests(arena, off, ln, threads=t), seconds, (1, pool_threads()))
         done1, dt1 = res[1]
         tp = max(res)
         return {
@@ -365,6 +417,7 @@ class MixedWorkload:
                       f"port of processor.go:133-143, SHA-NI compression",
             "pool": {"value": res[tp][0] * k / res[tp][1], "threads": tp},
             "cpu": _cpu_model(),
+            **_cpu_facts(),
         }
 
     def config_fields(self):
@@ -439,8 +492,7 @@ class EpochChangeWorkload:
         arena = self.buf[: k * self.plen]
         off = np.arange(k, dtype=np.uint64) * self.plen
         ln = np.full(k, self.plen, dtype=np.uint32)
-        res = _time_cpu(lambda t: o.hash_requests(arena, off, ln, threads=t), seconds,
-                        (1, min(16, os.cpu_count() or 1)))
+        res = _time_cpu(lambda t: o.hash_requests(arena, off, ln, threads=t), seconds, (1, pool_threads()))
         done1, dt1 = res[1]
         tp = max(res)
         return {
@@ -449,6 +501,7 @@ class EpochChangeWorkload:
                       f"of processor.go:133-143 (every ack hashed, as the reference does), SHA-NI compression",
             "pool": {"value": res[tp][0] * k / res[tp][1], "threads": tp},
             "cpu": _cpu_model(),
+            **_cpu_facts(),
         }
 
     def config_fields(self):
@@ -492,6 +545,18 @@ def main():
     for _ in range(a.warmup):
         wl.step()
     torch.cuda.synchronize(dev)
+    # Untimed pre-warm: the same steps until prewarm_ms of wall time have
+    # passed, so the timed region starts at the clock the chip holds under
+    # this load (DVFS; MI355X_MICROARCH.md).  Reported in the JSON line.
+    prewarm_steps, t_pw = 0, time.perf_counter()
+    while a.prewarm_ms > 0 and (time.perf_counter() - t_pw) * 1e3 < a.prewarm_ms:
+        for _ in range(8):
+            wl.step()
+        prewarm_steps += 8
+        torch.cuda.synchronize(dev)
+    prewarm_ms = (time.perf_counter() - t_pw) * 1e3
+    if dist:
+        dist.barrier()
 
     def timed(with_events):
         eng.set_timing(with_events)
@@ -510,7 +575,7 @@ def main():
         return el
 
     if a.timed_kernels == "dominant":
-        eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED, KERNEL_CONT])
+        eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED])
     dt = timed(bool(a.events_in_timed_loop))
     if not a.events_in_timed_loop:
         timed(True)
@@ -521,6 +586,13 @@ def main():
         # line's extras); the value and the roofline come from the pass above.
         eng.set_timing_mask(range(32))
         timed(True)
+
+    # Clock probe right behind the timed region (chip still at its load clock):
+    # register-only compressions in the request kernel's round form.
+    probe = None
+    if a.probe_iters > 0:
+        ghz, cyc = eng.clock_probe(a.probe_iters)
+        probe = {"clock_ghz": ghz, "cycles_per_wave_compression": cyc}
 
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -536,13 +608,19 @@ def main():
     achieved_tops = work_blocks * OPS_PER_COMPRESSION / (ms_per_step_k * 1e-3) / 1e12
     hbm_gbs = hbm_bytes / (ms_per_step_k * 1e-3) / 1e9
 
-    traffic = None
-    if os.path.exists(a.traffic_file):
-        try:
-            tf = json.load(open(a.traffic_file))
-            traffic = tf.get(f"config{a.config}", {}).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    tkey = kernel_source_key(a.variant)
+    traffic, tentry = lookup_traffic(a.traffic_file, tkey, a.config)
+    # Measured ceiling: the probe's register-only compression rate on this box
+    # (1,024 SIMDs x 64 lanes per wave-compression) and the clock it ran at.
+    measured = None
+    if probe and probe["cycles_per_wave_compression"] > 0:
+        ceil_cps = 1024 * 64 * probe["clock_ghz"] * 1e9 / probe["cycles_per_wave_compression"]
+        achieved_cps = work_blocks / (ms_per_step_k * 1e-3)
+        measured = {"compressions_per_s": ceil_cps, "frac": achieved_cps / ceil_cps,
+                    "cycles_per_wave_compression": probe["cycles_per_wave_compression"],
+                    "spec_cycles_per_wave_compression": 2 * OPS_PER_COMPRESSION,
+                    "note": "clock probe: 8 waves/SIMD of register-only compressions (the request kernel's "
+                            "round form), right after the timed region"}
 
     cpu = wl.cpu_baseline(a.cpu_seconds) if rank == 0 and world == 1 and a.cpu_seconds > 0 else None
 
@@ -564,8 +642,7 @@ def main():
                 "workload": f"config{a.config}: {wl.desc}",
                 **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": ["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only", "pair", "lds_pf",
-                                   "lds_old"][a.variant],
+                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair"}[a.variant],
             },
             "gb_per_s_hashed": gbps,
             "roofline": {
@@ -583,8 +660,16 @@ def main():
                         f"(over {n_k // a.steps} launch(es))",
                 "hbm_algorithmic_gb_per_s": hbm_gbs,
                 "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
-                "note": "SHA-256 is int32 VALU work (no MFMA shape); hbm/mfma bounds do not apply",
+                "traffic_key": tkey,
+                "traffic_source": (tentry or {}).get("source"),
+                "traffic_over_algorithmic": (traffic / hbm_bytes) if traffic else None,
+                "measured_peak": measured,
+                "note": "SHA-256 is int32 VALU work (no MFMA shape); hbm/mfma bounds do not apply; "
+                        "traffic = PMC HBM bytes per launch of this exact kernel source (null if not profiled)",
             },
+            "prewarm_ms": prewarm_ms,
+            "prewarm_steps": prewarm_steps,
+            "effective_clock_ghz": probe["clock_ghz"] if probe else None,
             **wl.extra(),
             "events_in_timed_loop": bool(a.events_in_timed_loop),
             "timed_kernels": a.timed_kernels,

@@ -71,26 +71,22 @@ const char* mirsha_last_error(const mirsha_ctx* ctx);
 int mirsha_ctx_set_stream(mirsha_ctx* ctx, void* hip_stream);
 void* mirsha_ctx_stream(mirsha_ctx* ctx);
 
-/* Kernel variant for sha256 over packed messages (A/B measurement):
+/* Kernel form for sha256 over packed messages (A/B measurement):
  * 0 = LDS-staged coalesced loader + generated-asm rounds (default; a launch
  *     of at most 512 64-message groups takes the producer/consumer pair
  *     kernel -- schedule and rounds of each compression on two waves on two
  *     SIMDs -- and one of at most 1024 groups (one wave per SIMD) the
  *     low-occupancy kernel: prefetching direct loads, no-yield rounds;
  *     MIRSHA_PAIR=0 in the environment disables the pair forms),
- * 1 = direct per-lane loads + asm rounds, 2 = LDS loader + compiler-scheduled
- * C++ rounds, 3 = direct loads + C++ rounds, 4 = the low-occupancy kernel at
- * any size, 5 = the LDS kernel at any size, 6 = the pair kernel at any size,
- * 7 = LDS loader with the next block's loads in flight during the rounds,
- * 8 = the round-1 LDS loader (per-chunk activity/range tests, 72 VGPRs).
- * All are bit-exact. */
+ * 1 = direct per-lane loads, 4 = the low-occupancy kernel at any size,
+ * 5 = the LDS kernel at any size, 6 = the pair kernel at any size.
+ * All are bit-exact.  2, 3, 7, 8 (round-1 A/B forms) are retired: EINVAL. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
 /* Per-kernel device-time accounting with HIP events on the launch stream.
- * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator,
- * 3 = pipelined batch-chain segments (on the context's second stream),
- * 4 = fused request -> batch kernel (one persistent launch per run),
- * 5 = continuation request -> batch kernel (MIRSHA_PIPELINE_CONT).
+ * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator
+ * and clock probe, 3 = batch-chain kernel, 4 = fused request -> batch kernel
+ * (one persistent launch per run).
  * set_timing_mask: bit k on = kernel k is timed while timing is enabled
  * (default: all); each timed launch adds two event records to its stream. */
 int mirsha_ctx_set_timing(mirsha_ctx* ctx, int enable);
@@ -227,27 +223,16 @@ int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, uint32
  *     chains (VerifyBatch of hundreds of digests).
  *   MIRSHA_PIPELINE_SEQUENTIAL: request kernel at full occupancy, then the
  *     list kernel.  Best for many short lists (BatchSize 20).
- *   MIRSHA_PIPELINE_STREAMS: requests in needed-at chunks with batch-chain
- *     segments on a second stream (midstate carried on device); measured
- *     slower at BASELINE sizes, kept for A/B.
- *   MIRSHA_PIPELINE_CONT: ONE launch at full occupancy for many short lists
- *     that are contiguous request ranges (the batches of a cycle in origin
- *     order; BatchSize a multiple of 4, >= 8).  Requests are hashed segment by
- *     segment (ordinals [0,8), [8,16), [16,20) at BatchSize 20); the request
- *     wave that completes a (64-list group, segment) counter hashes that
- *     segment's blocks itself, so batch chains advance beside later request
- *     tiles and only the last 2-3 blocks trail the launch.  Other shapes fall
- *     back to SEQUENTIAL (mirsha_pipeline_mode() reports it).
  *   MIRSHA_PIPELINE_AUTO (default): FUSED when the longest list is >= 64
  *     blocks (~126 digests) and there are <= 64 list groups, else SEQUENTIAL;
  *     mirsha_pipeline_mode() reports the choice.
+ * (Modes 2 and 4 -- chain segments on a second stream, and an in-kernel
+ * continuation form -- were measured slower and are retired: EINVAL.)
  * mirsha_pipeline_create reads MIRSHA_PIPELINE_MODE (auto | fused |
- * sequential | streams | cont; default auto). */
+ * sequential; default auto). */
 #define MIRSHA_PIPELINE_SEQUENTIAL 0
 #define MIRSHA_PIPELINE_FUSED 1
-#define MIRSHA_PIPELINE_STREAMS 2
 #define MIRSHA_PIPELINE_AUTO 3
-#define MIRSHA_PIPELINE_CONT 4
 typedef struct mirsha_pipeline mirsha_pipeline;
 int mirsha_pipeline_create(mirsha_ctx* ctx, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
                            const uint32_t* list_first, uint32_t n_lists, mirsha_pipeline** out);
@@ -266,11 +251,8 @@ int mirsha_pipeline_status(mirsha_ctx* ctx, mirsha_pipeline* p);
  * [2 n_tiles + n_counters + g].  *words = total length (0 when tracing is off). */
 int mirsha_pipeline_trace(mirsha_ctx* ctx, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words);
 int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t* n_counters, uint32_t* n_groups);
-/* Number of chain segments; bounds (optional, cap entries) = first ordinal of each. */
-int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap);
 /* Device-resident run: request digests to d_req_out (origin order), batch
- * digests to d_batch_out; asynchronous on the context stream (which is made to
- * wait for the chain stream before returning). */
+ * digests to d_batch_out; asynchronous on the context stream. */
 int mirsha_hash_requests_then_batches_device(mirsha_ctx* ctx, mirsha_pipeline* p, const uint8_t* d_arena,
                                              uint64_t arena_len, const uint64_t* d_off, const uint32_t* d_len,
                                              uint8_t* d_req_out, uint8_t* d_batch_out);
@@ -324,6 +306,16 @@ int mirsha_synth_mixed_lengths_device(mirsha_ctx* ctx, uint64_t seed, uint64_t f
                                       uint32_t* d_len);
 int mirsha_synth_mixed_device(mirsha_ctx* ctx, uint64_t seed, uint64_t first, uint64_t count,
                               const uint64_t* d_off, uint8_t* d_arena);
+
+/* Clock probe (diagnostics; bench.py runs it right after its timed region):
+ * every SIMD runs 8 waves of `iters` back-to-back register-only compressions
+ * in the request kernel's round form.  *clock_ghz = median over waves of
+ * shader cycles / 100 MHz reference ticks (the clock held under this load);
+ * *cycles_per_wave_compression = launch span (first wave start to last wave
+ * end, in shader cycles at that clock) / (iters x 8): the SIMD cycles one
+ * 64-lane compression costs with no memory traffic at all (the measured
+ * ceiling the request kernel is compared with).  Synchronous. */
+int mirsha_clock_probe(mirsha_ctx* ctx, uint32_t iters, double* clock_ghz, double* cycles_per_wave_compression);
 
 #ifdef __cplusplus
 }

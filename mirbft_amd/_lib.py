@@ -82,7 +82,6 @@ SIGNATURES = {
     "mirsha_pipeline_status": (c_int, [c_void_p, c_void_p]),
     "mirsha_pipeline_trace": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "mirsha_pipeline_shape": (c_int, [c_void_p, _u32p, _u32p, _u32p]),
-    "mirsha_pipeline_segments": (c_int, [c_void_p, _u32p, c_void_p, c_uint32]),
     "mirsha_hash_requests_then_batches_device": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p],
@@ -99,6 +98,7 @@ SIGNATURES = {
     "mirsha_synth_requests_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint32, c_void_p]),
     "mirsha_synth_mixed_lengths_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p]),
     "mirsha_synth_mixed_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p]),
+    "mirsha_clock_probe": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
 }
 
 
@@ -119,12 +119,15 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    # MIRSHA_AB_LIB: an A/B build of the same sources (tools/ab_build.sh) for
+    # same-box timing comparisons; never set by tests, smoke() or the driver.
+    path = os.environ.get("MIRSHA_AB_LIB") or LIB_PATH
+    if not os.path.exists(path):
         raise MirshaUnavailable(
             f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(hipcc --offload-arch=gfx950).  There is no CPU fallback."
         )
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res

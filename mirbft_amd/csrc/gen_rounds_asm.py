@@ -30,6 +30,7 @@ filler gives nearly the same (5,041), two fillers or `s_nop 1` lose, and a
 filler after the 2-cycle-class ops loses.
 
 Run:  python gen_rounds_asm.py > sha256_rounds_asm.h
+      python gen_rounds_asm.py --ab > ../../tools/sha256_rounds_asm_ab.h
 """
 
 K = [
@@ -67,8 +68,14 @@ def yield_after_complex(lines):
 
 
 def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr", nops=False):
-    lines = []
+    """8 rounds from j0.  k_mode: "sgpr" = K[j] as 8 SGPR inputs %28..%35 (the
+    compiler hoists all 64 constants out of a block loop: 64 live SGPRs);
+    "smov" = K[j] written by s_mov_b32 into ONE scratch SGPR output %28 inside
+    the statement, in the slot of the round's first issue-yield s_nop (the
+    scalar move yields the VALU slot just like the nop); "lit" = VOP2 literal."""
+    rounds = []
     for r in range(8):
+        lines = []
         j = j0 + r
         a, b, c, d, e, f, g, h = [op(STATE[(k - r) % 8]) for k in range(8)]
         wj = op(W[j & 15])
@@ -104,8 +111,8 @@ def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr", nops=False):
             lines.append(f"v_add3_u32 {h}, {h}, {t0}, {t1}")
         else:
             lines += [f"v_add_u32_e32 {h}, {h}, {t0}", f"v_add_u32_e32 {h}, {h}, {t1}"]
-        if k_mode == "sgpr":
-            lines.append(f"v_add3_u32 {h}, {h}, {op(KOP[r])}, {wj}")
+        if k_mode in ("sgpr", "smov"):
+            lines.append(f"v_add3_u32 {h}, {h}, {op(KOP[r]) if k_mode == 'sgpr' else op(KOP[0])}, {wj}")
         else:  # VOP2 with a 32-bit literal: h += K, h += W
             lines += [f"v_add_u32_e32 {h}, 0x{K[j]:08x}, {h}", f"v_add_u32_e32 {h}, {h}, {wj}"]
         lines += [
@@ -120,7 +127,18 @@ def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr", nops=False):
             lines.append(f"v_add3_u32 {h}, {h}, {t0}, {t1}")
         else:
             lines += [f"v_add_u32_e32 {h}, {h}, {t0}", f"v_add_u32_e32 {h}, {h}, {t1}"]
-    return yield_after_complex(lines) if nops else lines
+        if nops:
+            lines = yield_after_complex(lines)
+        if k_mode == "smov":
+            # K[j] into the scratch SGPR: in the slot of the round's first
+            # yield with nops (after its first 4-cycle op), else up front.
+            mov = f"s_mov_b32 {op(KOP[0])}, 0x{K[j]:08x}"
+            if nops:
+                lines[lines.index("s_nop 0")] = mov
+            else:
+                lines.insert(0, mov)
+        rounds += lines
+    return rounds
 
 
 def block_ilp(j0):
@@ -232,10 +250,16 @@ def emit_fn_kw(name):
     return out
 
 
+# Product forms (sha256_rounds_asm.h): the request kernel's yield form and
+# the latency form of the lone-wave chains.
 VARIANTS = {
     # name: (ch_mode, add_mode, k_mode, nops)
-    "rounds_asm": ("bitop3", "add3", "sgpr", True),
+    "rounds_asm": ("bitop3", "add3", "smov", True),
     "rounds_asm_nonop": ("bitop3", "add3", "sgpr", False),
+}
+# A/B forms for tools/ only (tools/sha256_rounds_asm_ab.h), bit-identical.
+AB_VARIANTS = {
+    "rounds_asm_ksgpr": ("bitop3", "add3", "sgpr", True),
     "rounds_asm_bfi": ("bfi", "add3", "sgpr", False),
     "rounds_asm_add2": ("bitop3", "add", "sgpr", False),
     "rounds_asm_lit": ("bitop3", "add3", "lit", False),
@@ -245,7 +269,7 @@ VARIANTS = {
 
 def emit_fn(name, ch_mode, add_mode, k_mode, nops):
     out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16]) {{",
-           "    uint32_t t0, t1, t2, t3;"]
+           "    uint32_t t0, t1, t2, t3;" + (" uint32_t kt;" if k_mode == "smov" else "")]
     for j0 in range(0, 64, 8):
         body = block(j0, ch_mode, add_mode, k_mode, nops)
         out.append(f"    // rounds {j0}..{j0 + 7}")
@@ -253,7 +277,8 @@ def emit_fn(name, ch_mode, add_mode, k_mode, nops):
         for ln in body:
             out.append(f'        "{ln}\\n\\t"')
         outs = ", ".join([f'"+v"(s[{i}])' for i in range(8)] + [f'"+v"(w[{i}])' for i in range(16)]
-                         + ['"=&v"(t0)', '"=&v"(t1)', '"=&v"(t2)', '"=&v"(t3)'])
+                         + ['"=&v"(t0)', '"=&v"(t1)', '"=&v"(t2)', '"=&v"(t3)']
+                         + (['"=&s"(kt)'] if k_mode == "smov" else []))
         if k_mode == "sgpr":
             ins = ", ".join(f'"s"(0x{K[j0 + r]:08X}u)' for r in range(8))
         else:
@@ -265,23 +290,27 @@ def emit_fn(name, ch_mode, add_mode, k_mode, nops):
     return out
 
 
+HEADER = [
+    "// GENERATED by mirbft_amd/csrc/gen_rounds_asm.py — do not edit by hand.",
+    "// 64 SHA-256 rounds (FIPS 180-4 §6.2.2) for gfx950, 8 per asm statement.",
+]
+
+
 def emit():
-    out = []
-    out.append("// GENERATED by gen_rounds_asm.py — do not edit by hand.")
-    out.append("// 64 SHA-256 rounds (FIPS 180-4 §6.2.2) for gfx950, 8 per asm statement.")
-    out.append("// rounds_asm is the production form; the others exist for A/B timing")
-    out.append("// (tools/valu_microbench.hip) and are bit-identical in result.")
-    out.append("#pragma once")
-    out.append("#include <stdint.h>")
-    out.append("")
-    out.append("namespace mirsha {")
-    out.append("")
-    out.append("// s[0..7] = working variables a..h (updated in place: after 8 rounds the")
-    out.append("// names have rotated back), w[0..15] = schedule window (consumed).")
+    out = HEADER + [
+        "// rounds_asm: throughput form (issue-yield s_nop after each 4-cycle op, K[j]",
+        "// by s_mov_b32 into one scratch SGPR in a yield slot, so no constants stay",
+        "// live across a block loop); rounds_asm_nonop: latency form (lone waves).",
+        "#pragma once",
+        "#include <stdint.h>",
+        "",
+        "namespace mirsha {",
+        "",
+        "// s[0..7] = working variables a..h (updated in place: after 8 rounds the",
+        "// names have rotated back), w[0..15] = schedule window (consumed).",
+    ]
     for name, (ch, ad, km, nops) in VARIANTS.items():
         out += emit_fn(name, ch, ad, km, nops)
-    out.append("// Latency-oriented order (lone waves): same instructions, 12 temporaries.")
-    out += emit_fn_ilp("rounds_asm_ilp")
     out.append("// 8 consumer rounds with K + W precomputed (pair kernels): names rotate")
     out.append("// back after 8 rounds, so the same statement serves every 8-round chunk.")
     out += emit_fn_kw("rounds_kw8_asm")
@@ -289,7 +318,25 @@ def emit():
     return "\n".join(out) + "\n"
 
 
+def emit_ab():
+    out = HEADER + [
+        "// A/B timing forms for tools/ (valu_microbench.hip), bit-identical to the",
+        "// product forms in mirbft_amd/csrc/sha256_rounds_asm.h.",
+        "#pragma once",
+        "#include <stdint.h>",
+        "",
+        "namespace mirsha {",
+        "",
+    ]
+    for name, (ch, ad, km, nops) in AB_VARIANTS.items():
+        out += emit_fn(name, ch, ad, km, nops)
+    out.append("// Latency-oriented order (lone waves): same instructions, 12 temporaries.")
+    out += emit_fn_ilp("rounds_asm_ilp")
+    out.append("}  // namespace mirsha")
+    return "\n".join(out) + "\n"
+
+
 if __name__ == "__main__":
     import sys
 
-    sys.stdout.write(emit())
+    sys.stdout.write(emit_ab() if "--ab" in sys.argv else emit())

@@ -103,8 +103,7 @@ struct mirsha_ctx {
     std::string err;
     DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
     PinnedBuf h_stage;
-    KernelTimer timers[6];         // msgs, lists, gen, chain, fused, cont
-    hipStream_t chain_stream = nullptr;  // dependent-pass stream of the pipeline (lazy)
+    KernelTimer timers[6];         // msgs, lists, gen, chain, fused, (5: retired)
     AsyncSlot slots[kAsyncSlots];
     uint64_t next_ticket = 1;  // ticket of the next submission
     uint64_t done_ticket = 0;  // every ticket <= this one has completed
@@ -134,15 +133,7 @@ struct mirsha_pipeline {
     bool trace = false;
     std::vector<uint32_t> cidx, cfirst;      // compacted lists (no null entries)
     std::vector<uint32_t> order;             // request processing order
-    std::vector<uint32_t> chunk_begin;       // per chunk: first position in `order`; size n_chunks + 1
-    std::vector<uint32_t> seg_bound;         // segment s covers ordinals [seg_bound[s], seg_bound[s+1])
-    std::vector<hipEvent_t> chunk_done;      // one per chain segment
-    hipEvent_t chain_done = nullptr;
     DevBuf d_cidx, d_cfirst, d_order, d_state;
-    // continuation mode (sha256_msgs_cont_kernel)
-    std::vector<uint32_t> ctarget;
-    uint32_t cont_flags = 0;                 // mirsha::kContLatFinal (MIRSHA_CONT_FLAGS)
-    DevBuf d_ctarget, d_cplan;
 };
 
 namespace {
@@ -352,65 +343,16 @@ int lists_resident(mirsha_ctx* c, const uint8_t* d_digests, uint32_t n_digests, 
     });
 }
 
-// ---- request -> batch-digest pipeline ------------------------------------
+// ---- request -> batch-digest plan (sequential form) ------------------------
 //
 // The dependent pass (batch / VerifyBatch digests over request digests,
 // sequence.go:154-157, batch_tracker.go:147-150) is a set of sequential SHA
-// chains: list k's block b needs only digests 2b and 2b+1.  Requests are
-// therefore hashed in "needed-at" order (their smallest ordinal in any list)
-// in chunks, and each chunk is followed — on a second stream — by one chain
-// SEGMENT that advances every list over the ordinals that chunk completed
-// (midstate carried in d_state).  Segment s runs beside request chunk s+1;
-// only the last segment (<= 2 compressions when the chain is short) is exposed.
-
-constexpr double kChainSecondsPerCompression = 3.0e-6;  // chain wave beside request waves
-constexpr double kRequestCompressionsPerSecond = 21.0e9;
-
-// Measured on MI355X (profiles/r01/pipeline_timeline.txt): a cross-stream
-// event hand-off costs ~17 us per chunk boundary, small request chunks are
-// latency-bound (a wave's own chain), and chain segments overlapped with 8
-// request waves per SIMD slow down ~4x despite s_setprio.  Stream-level
-// pipelining therefore loses at BASELINE sizes; the default plan is ONE
-// segment (request pass, then the chain pass).  MIRSHA_PIPELINE_SEGMENTS=auto
-// enables the cost-model split below for experiments.
-std::vector<uint32_t> plan_segments(uint32_t maxc, double request_seconds, bool split) {
-    std::vector<uint32_t> b{0};
-    if (!split || maxc <= 2) return b;
-    const uint32_t top = maxc & ~1u;  // last even ordinal <= maxc
-    const double r = request_seconds / maxc;                // request time per ordinal
-    const double h = kChainSecondsPerCompression / 2.0;     // chain time per ordinal
-    if (h * 2.0 < r) {
-        // Chain much faster than requests: widths grow backwards from a
-        // 2-ordinal tail so that each segment hides behind the next chunk.
-        std::vector<uint32_t> w{2};
-        uint32_t sum = 2;
-        while (sum < top && w.size() < 3) {
-            uint32_t nw = (uint32_t)(w.back() * r / h) & ~1u;
-            if (nw < 2) nw = 2;
-            if (sum + nw > top || w.size() == 2) nw = top - sum;  // first segment takes the rest
-            w.push_back(nw);
-            sum += nw;
-        }
-        uint32_t acc = 0;
-        for (size_t i = w.size(); i-- > 1;) {
-            acc += w[i];
-            b.push_back(acc);
-        }
-    } else {
-        // Chain-bound: start the chain early (small first chunk), then equal segments.
-        const uint32_t S = std::min<uint32_t>(8, top / 2);
-        uint32_t first = ((top / (2 * S)) + 1) & ~1u;
-        if (first < 2) first = 2;
-        b.push_back(first);
-        const uint32_t rest = top - first;
-        for (uint32_t s = 1; s < S && rest; s++) {
-            const uint32_t v = (first + (uint32_t)((uint64_t)rest * s / (S - 1))) & ~1u;
-            if (v > b.back() && v < top) b.push_back(v);
-        }
-    }
-    return b;
-}
-
+// chains over the request digests.  The sequential plan runs the request
+// kernel at full occupancy, then the list chains; the lists are compacted
+// once per plan (null requests contribute no bytes and are dropped).
+// Stream-level pipelining (chain segments on a second stream) and the
+// in-kernel continuation form were measured slower at BASELINE sizes and
+// removed (code in git history before round 2).
 int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t* idx, const uint32_t* first,
                    uint32_t n_lists, const uint32_t* len) {
     p->n_req = n_req;
@@ -418,52 +360,24 @@ int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint
     p->cfirst.assign(n_lists + 1, 0);
     p->cidx.clear();
     p->cidx.reserve(first[n_lists]);
-    std::vector<uint32_t> needed(n_req, UINT32_MAX);
-    uint32_t maxc = 0;
+    std::vector<uint8_t> listed(n_req, 0);
     for (uint32_t k = 0; k < n_lists; k++) {
-        uint32_t ord = 0;
         for (uint32_t e = first[k]; e < first[k + 1]; e++) {
             if (idx[e] == MIRSHA_NULL_INDEX) continue;  // empty digest: contributes no bytes
             p->cidx.push_back(idx[e]);
-            needed[idx[e]] = std::min(needed[idx[e]], ord);
-            ord++;
+            listed[idx[e]] = 1;
         }
         p->cfirst[k + 1] = (uint32_t)p->cidx.size();
-        maxc = std::max(maxc, ord);
     }
     p->n_entries = (uint32_t)p->cidx.size();
-    double comps = 0;
-    for (uint32_t i = 0; i < n_req; i++) comps += len ? host_blocks(len[i]) : 5.0;
-    p->seg_bound = plan_segments(maxc, comps / kRequestCompressionsPerSecond, p->mode == MIRSHA_PIPELINE_STREAMS);
-    const uint32_t S = (uint32_t)p->seg_bound.size();
-    // chunk id: segment whose ordinal range holds needed-at; unlisted last (S)
-    auto chunk_of = [&](uint32_t r) -> uint32_t {
-        const uint32_t n = needed[r];
-        if (n == UINT32_MAX) return S;
-        uint32_t s = (uint32_t)(std::upper_bound(p->seg_bound.begin(), p->seg_bound.end(), n) - p->seg_bound.begin()) - 1;
-        return s;
-    };
-    std::vector<uint32_t> cid(n_req);
-    std::vector<uint32_t> cnt(S + 2, 0);
-    for (uint32_t r = 0; r < n_req; r++) {
-        cid[r] = chunk_of(r);
-        cnt[cid[r] + 1]++;
-    }
-    p->chunk_begin.assign(S + 2, 0);
-    for (uint32_t s = 0; s <= S; s++) p->chunk_begin[s + 1] = p->chunk_begin[s] + cnt[s + 1];
-    p->order.assign(n_req, 0);
-    std::vector<uint32_t> pos(p->chunk_begin.begin(), p->chunk_begin.end() - 1);
-    // stable by chunk; within a chunk longest-first by block count (length bucketing)
-    std::vector<uint32_t> byc(n_req);
-    for (uint32_t r = 0; r < n_req; r++) byc[pos[cid[r]]++] = r;
-    if (len) {
-        for (uint32_t s = 0; s <= S; s++) {
-            auto b = byc.begin() + p->chunk_begin[s], e = byc.begin() + p->chunk_begin[s + 1];
-            std::stable_sort(b, e, [&](uint32_t x, uint32_t y) { return host_blocks(len[x]) > host_blocks(len[y]); });
-        }
-    }
-    p->order = std::move(byc);
-    // device copies
+    // Processing order: listed requests first, then longest-first by block
+    // count (length bucketing inside a wave), stable.
+    p->order.resize(n_req);
+    for (uint32_t r = 0; r < n_req; r++) p->order[r] = r;
+    std::stable_sort(p->order.begin(), p->order.end(), [&](uint32_t x, uint32_t y) {
+        if (listed[x] != listed[y]) return listed[x] > listed[y];
+        return len ? host_blocks(len[x]) > host_blocks(len[y]) : false;
+    });
     HIP_TRY(c, p->d_cidx.ensure(sizeof(uint32_t) * std::max<uint32_t>(p->n_entries, 1)));
     HIP_TRY(c, p->d_cfirst.ensure(sizeof(uint32_t) * (n_lists + 1)));
     HIP_TRY(c, p->d_order.ensure(sizeof(uint32_t) * std::max<uint32_t>(n_req, 1)));
@@ -476,68 +390,30 @@ int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint
     if (n_req)
         HIP_TRY(c, hipMemcpyAsync(p->d_order.p, p->order.data(), sizeof(uint32_t) * n_req, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    p->chunk_done.resize(S, nullptr);
-    for (auto& e : p->chunk_done)
-        if (!e) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (!p->chain_done) HIP_TRY(c, hipEventCreateWithFlags(&p->chain_done, hipEventDisableTiming));
     return MIRSHA_OK;
 }
 
 int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
                  const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
-    const uint32_t S = (uint32_t)p->seg_bound.size();
     const uint32_t* order = p->d_order.as<uint32_t>();
-    if (S == 1) {
-        // Sequential: request kernel, then the list chains on the same stream.
-        const uint32_t n = p->chunk_begin[S + 1];
-        if (n) {
-            if (int rc = timed_launch(c, 0, [&] {
-                    return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, order, n, d_req_out,
-                                               c->variant, c->stream);
-                }))
-                return rc;
-        }
-        if ((p->n_lists + 63u) / 64u <= mirsha::pair_max_groups())
-            return timed_launch(c, 1, [&] {  // few long chains: producer/consumer pairs
-                return mirsha::launch_chain_pair(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
-                                                 p->d_cfirst.as<uint32_t>(), p->n_lists, d_list_out, c->stream);
-            });
-        return timed_launch(c, 1, [&] {
-            return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
-                                        p->d_cfirst.as<uint32_t>(), p->n_lists, 0u, mirsha::kOpenEnd,
-                                        p->d_state.as<uint32_t>(), d_list_out, c->stream);
-        });
-    }
-    if (!c->chain_stream) HIP_TRY(c, hipStreamCreateWithFlags(&c->chain_stream, hipStreamNonBlocking));
-    // The chain stream must not start a new run before the caller's stream
-    // reached it (previous consumers of d_req_out/d_list_out on that stream).
-    HIP_TRY(c, hipEventRecord(p->chain_done, c->stream));
-    HIP_TRY(c, hipStreamWaitEvent(c->chain_stream, p->chain_done, 0));
-    for (uint32_t s = 0; s <= S; s++) {
-        const uint32_t b = p->chunk_begin[s], n = p->chunk_begin[s + 1] - b;
-        if (n) {
-            if (int rc = timed_launch(c, 0, [&] {
-                    return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, order + b, n, d_req_out,
-                                               c->variant, c->stream);
-                }))
-                return rc;
-        }
-        if (s == S) break;  // unlisted requests: no chain segment depends on them
-        HIP_TRY(c, hipEventRecord(p->chunk_done[s], c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->chain_stream, p->chunk_done[s], 0));
-        const uint32_t ob = p->seg_bound[s];
-        const uint32_t oe = s + 1 < S ? p->seg_bound[s + 1] : mirsha::kOpenEnd;
-        if (int rc = timed_launch_on(c, 3, c->chain_stream, [&] {
-                return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
-                                            p->d_cfirst.as<uint32_t>(), p->n_lists, ob, oe,
-                                            p->d_state.as<uint32_t>(), d_list_out, c->chain_stream);
+    if (p->n_req) {
+        if (int rc = timed_launch(c, 0, [&] {
+                return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, order, p->n_req, d_req_out, c->variant,
+                                           c->stream);
             }))
             return rc;
     }
-    // Join: the caller's stream waits for the last chain segment.
-    HIP_TRY(c, hipEventRecord(p->chain_done, c->chain_stream));
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, p->chain_done, 0));
-    return MIRSHA_OK;
+    if (p->n_lists == 0) return MIRSHA_OK;
+    if ((p->n_lists + 63u) / 64u <= mirsha::pair_max_groups())
+        return timed_launch(c, 1, [&] {  // few long chains: producer/consumer pairs
+            return mirsha::launch_chain_pair(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
+                                             p->d_cfirst.as<uint32_t>(), p->n_lists, d_list_out, c->stream);
+        });
+    return timed_launch(c, 1, [&] {
+        return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
+                                    p->d_cfirst.as<uint32_t>(), p->n_lists, 0u, mirsha::kOpenEnd,
+                                    p->d_state.as<uint32_t>(), d_list_out, c->stream);
+    });
 }
 
 
@@ -710,184 +586,6 @@ int fused_status(mirsha_ctx* c, mirsha_pipeline* p) {
     return MIRSHA_OK;
 }
 
-// ---- continuation plan: one request launch, list segments ride on it --------
-//
-// Admitted shape (else the plan falls back to SEQUENTIAL): contiguous lists
-// from request 0 with no null entries (list k = requests [first[k],
-// first[k+1]): the batches of one Ready() cycle in origin order,
-// sequence.go:154-157), every list B requests but the last (1..B), B a
-// multiple of 4 and >= 8, so that with segment bounds on multiples of 4 no
-// 128-byte line of request digests feeds two (group, segment) pairs.
-bool cont_shape(const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint32_t n_req, uint32_t* B) {
-    if (n_lists == 0 || first[0] != 0) return false;
-    const uint32_t b = first[1] - first[0];
-    if (b < 8 || b % 4u != 0 || first[n_lists] > n_req) return false;
-    for (uint32_t k = 0; k < n_lists; k++) {
-        const uint32_t c = first[k + 1] - first[k];
-        if (k + 1 < n_lists ? c != b : (c == 0 || c > b)) return false;
-    }
-    for (uint32_t e = 0; e < first[n_lists]; e++)
-        if (idx[e] != e) return false;
-    *B = b;
-    return true;
-}
-
-// Segment bounds (ordinals, multiples of 4): the last segment holds the last
-// 4 ordinals (2 digest blocks + the padding block trail the launch), the rest
-// is split in two.  MIRSHA_CONT_BOUNDS="8,16" overrides (A/B).
-std::vector<uint32_t> cont_bounds(uint32_t B) {
-    std::vector<uint32_t> b{0};
-    if (const char* e = getenv("MIRSHA_CONT_BOUNDS")) {
-        for (const char* s = e; *s;) {
-            char* end = nullptr;
-            const uint32_t v = (uint32_t)strtoul(s, &end, 10);
-            if (end == s) break;
-            if (v > b.back() && v < B && v % 4u == 0 && b.size() < mirsha::kContMaxSegments) b.push_back(v);
-            s = *end ? end + 1 : end;
-        }
-        return b;
-    }
-    const uint32_t last = B - 4u;
-    const uint32_t mid = (last / 2u) & ~3u;
-    if (mid > 0) b.push_back(mid);
-    if (last > b.back()) b.push_back(last);
-    return b;
-}
-
-int cont_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t* first, uint32_t n_lists, uint32_t B) {
-    p->n_req = n_req;
-    p->n_lists = n_lists;
-    p->n_entries = first[n_lists];
-    p->cfirst.assign(first, first + n_lists + 1);
-    p->seg_bound = cont_bounds(B);
-    const uint32_t S = (uint32_t)p->seg_bound.size();
-    auto seg_of = [&](uint32_t o) -> uint32_t {
-        return (uint32_t)(std::upper_bound(p->seg_bound.begin(), p->seg_bound.end(), o) - p->seg_bound.begin()) - 1u;
-    };
-    // Processing order: segment of the ordinal (unlisted requests last), then
-    // request index.
-    const uint32_t listed = first[n_lists];
-    std::vector<uint32_t> cnt(S + 2, 0);
-    for (uint32_t r = 0; r < n_req; r++) cnt[(r < listed ? seg_of(r % B) : S) + 1]++;
-    for (uint32_t s = 0; s <= S; s++) cnt[s + 1] += cnt[s];
-    const std::vector<uint32_t> seg_first(cnt.begin(), cnt.end());  // first position of each segment
-    p->order.assign(n_req, 0);
-    std::vector<uint32_t> pos_of(n_req);
-    for (uint32_t r = 0; r < n_req; r++) {
-        const uint32_t s = r < listed ? seg_of(r % B) : S;
-        pos_of[r] = cnt[s];
-        p->order[cnt[s]++] = r;
-    }
-    p->n_tiles = (n_req + 63u) / 64u;
-    p->n_groups = (n_lists + 63u) / 64u;
-    p->n_counters = p->n_groups * S;
-    std::vector<uint64_t> pairs;
-    pairs.reserve(listed / 8u + 1u);
-    for (uint32_t r = 0; r < listed; r++)
-        pairs.push_back(((uint64_t)(pos_of[r] >> 6) << 32) | ((r / B) / 64u * S + seg_of(r % B)));
-    std::sort(pairs.begin(), pairs.end());
-    pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
-    p->tadj_first.assign(p->n_tiles + 1, 0);
-    p->tadj.resize(pairs.size());
-    p->ctarget.assign(p->n_counters, 0);
-    for (size_t i = 0; i < pairs.size(); i++) {
-        p->tadj_first[(pairs[i] >> 32) + 1]++;
-        p->tadj[i] = (uint32_t)pairs[i];
-        p->ctarget[(uint32_t)pairs[i]]++;
-    }
-    for (uint32_t t = 0; t < p->n_tiles; t++) p->tadj_first[t + 1] += p->tadj_first[t];
-    for (uint32_t g = 0; g < p->n_groups; g++) {
-        if (p->ctarget[g * S] == 0) return fail(c, MIRSHA_EINVAL, "cont plan: group %u has no segment-0 tile", g);
-        for (uint32_t s = 1; s < S; s++) p->ctarget[g * S + s]++;  // + the previous segment's signal
-    }
-    p->cont_flags = 0;
-    if (const char* e = getenv("MIRSHA_CONT_FLAGS")) p->cont_flags = (uint32_t)atoi(e);
-    auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
-        HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
-        if (bytes) HIP_TRY(c, hipMemcpyAsync(d.p, h, bytes, hipMemcpyHostToDevice, c->stream));
-        return MIRSHA_OK;
-    };
-    if (int rc = up(p->d_cfirst, p->cfirst.data(), sizeof(uint32_t) * (n_lists + 1))) return rc;
-    if (int rc = up(p->d_order, p->order.data(), sizeof(uint32_t) * n_req)) return rc;
-    if (int rc = up(p->d_tadj_first, p->tadj_first.data(), sizeof(uint32_t) * (p->n_tiles + 1))) return rc;
-    if (int rc = up(p->d_tadj, p->tadj.data(), sizeof(uint32_t) * p->tadj.size())) return rc;
-    if (int rc = up(p->d_ctarget, p->ctarget.data(), sizeof(uint32_t) * p->ctarget.size())) return rc;
-    // Fallback of a misaligned output (cont_run): the chain kernel over the
-    // (identity) compacted lists.
-    p->cidx.resize(listed);
-    for (uint32_t e = 0; e < listed; e++) p->cidx[e] = e;
-    if (int rc = up(p->d_cidx, p->cidx.data(), sizeof(uint32_t) * listed)) return rc;
-    HIP_TRY(c, p->d_counters.ensure(8ull * std::max<uint32_t>(p->n_counters, 1)));
-    HIP_TRY(c, hipMemsetAsync(p->d_counters.p, 0, 8ull * std::max<uint32_t>(p->n_counters, 1), c->stream));
-    HIP_TRY(c, p->d_state.ensure(32ull * std::max<uint32_t>(S - 1u, 1u) * n_lists));
-    mirsha::ContPlan cp{};
-    cp.cfirst = p->d_cfirst.as<uint32_t>();
-    cp.tadj_first = p->d_tadj_first.as<uint32_t>();
-    cp.tadj = p->d_tadj.as<uint32_t>();
-    cp.ctarget = p->d_ctarget.as<uint32_t>();
-    cp.counters = p->d_counters.as<unsigned long long>();
-    cp.state = p->d_state.as<uint32_t>();
-    cp.n_lists = n_lists;
-    cp.n_seg = S;
-    cp.flags = p->cont_flags;
-    cp.n_tiles = p->n_tiles;
-    {
-        double frac = 0.3;
-        if (const char* e = getenv("MIRSHA_CONT_PRIO_FRAC")) frac = atof(e);
-        cp.prio_tile = (uint32_t)(frac * p->n_tiles);
-    }
-    const char* tr = getenv("MIRSHA_CONT_TRACE");
-    p->trace = tr && atoi(tr) != 0;
-    if (p->trace) {
-        const size_t words = 2ull * p->n_tiles + 2ull * p->n_counters;
-        HIP_TRY(c, p->d_trace.ensure(8ull * words));
-        HIP_TRY(c, hipMemsetAsync(p->d_trace.p, 0, 8ull * words, c->stream));
-        cp.trace = p->d_trace.as<unsigned long long>();
-    }
-    for (uint32_t s = 0; s < S; s++) {
-        cp.bound[s] = p->seg_bound[s];
-        cp.seg_tile[s] = seg_first[s] / 64u;
-    }
-    if (int rc = up(p->d_cplan, &cp, sizeof(cp))) return rc;
-    HIP_TRY(c, hipStreamSynchronize(c->stream));  // host vectors / cp outlive the copies
-    p->epoch = 0;
-    return MIRSHA_OK;
-}
-
-int cont_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
-             const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
-    if (p->n_req == 0) return MIRSHA_OK;
-    if ((reinterpret_cast<uintptr_t>(d_req_out) & 127u) != 0 || arena_len > mirsha::kMaxBufferArena) {
-        // The line-exclusivity argument needs 128-B aligned digests; the
-        // 32-bit loader needs the arena in one descriptor.  Two kernels.
-        if (int rc = timed_launch(c, 0, [&] {
-                return mirsha::launch_msgs(d_arena, arena_len, d_off, d_len, nullptr, p->n_req, d_req_out, c->variant,
-                                           c->stream);
-            }))
-            return rc;
-        return timed_launch(c, 1, [&] {
-            return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
-                                        p->d_cfirst.as<uint32_t>(), p->n_lists, 0u, mirsha::kOpenEnd,
-                                        p->d_state.as<uint32_t>(), d_list_out, c->stream);
-        });
-    }
-    mirsha::ContArgs a{};
-    a.arena = d_arena;
-    a.arena_len = arena_len;
-    a.off = d_off;
-    a.len = d_len;
-    a.order = p->d_order.as<uint32_t>();
-    a.req_out = d_req_out;
-    a.list_out = d_list_out;
-    a.plan = p->d_cplan.as<mirsha::ContPlan>();
-    a.n_req = p->n_req;
-    a.epoch = p->epoch + 1u;
-    a.flags = p->cont_flags;
-    if (int rc = timed_launch(c, 5, [&] { return mirsha::launch_cont(a, c->stream); })) return rc;
-    p->epoch++;
-    return MIRSHA_OK;
-}
-
 // AUTO: the fused launch pays when a few LONG chains would otherwise run after
 // the request pass (VerifyBatch of hundreds of digests, BASELINE config 3:
 // 1.49 -> 1.04 ms); many short lists (BatchSize 20, config 2) run better as
@@ -907,11 +605,6 @@ int plan_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t
                uint32_t n_lists, const uint32_t* len) {
     if (p->mode == MIRSHA_PIPELINE_AUTO)
         p->mode = fused_pays(idx, first, n_lists) ? MIRSHA_PIPELINE_FUSED : MIRSHA_PIPELINE_SEQUENTIAL;
-    if (p->mode == MIRSHA_PIPELINE_CONT) {
-        uint32_t B = 0;
-        if (cont_shape(idx, first, n_lists, n_req, &B)) return cont_build(c, p, n_req, first, n_lists, B);
-        p->mode = MIRSHA_PIPELINE_SEQUENTIAL;  // shape not admitted: two kernels
-    }
     if (p->mode == MIRSHA_PIPELINE_FUSED) return fused_build(c, p, n_req, idx, first, n_lists, len);
     return pipeline_build(c, p, n_req, idx, first, n_lists, len);
 }
@@ -919,23 +612,17 @@ int plan_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t
 int plan_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
              const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
     if (p->mode == MIRSHA_PIPELINE_FUSED) return fused_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
-    if (p->mode == MIRSHA_PIPELINE_CONT) return cont_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
     return pipeline_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_list_out);
 }
 
 int default_pipeline_mode() {
     const char* m = getenv("MIRSHA_PIPELINE_MODE");
     if (m && strcmp(m, "sequential") == 0) return MIRSHA_PIPELINE_SEQUENTIAL;
-    if (m && strcmp(m, "streams") == 0) return MIRSHA_PIPELINE_STREAMS;
     if (m && strcmp(m, "fused") == 0) return MIRSHA_PIPELINE_FUSED;
-    if (m && strcmp(m, "cont") == 0) return MIRSHA_PIPELINE_CONT;
     return MIRSHA_PIPELINE_AUTO;
 }
 
 void pipeline_free(mirsha_pipeline* p) {
-    for (auto e : p->chunk_done)
-        if (e) (void)hipEventDestroy(e);
-    if (p->chain_done) (void)hipEventDestroy(p->chain_done);
     p->d_cidx.release();
     p->d_cfirst.release();
     p->d_order.release();
@@ -947,8 +634,6 @@ void pipeline_free(mirsha_pipeline* p) {
     p->d_counters.release();
     p->d_ctl.release();
     p->d_trace.release();
-    p->d_ctarget.release();
-    p->d_cplan.release();
 }
 
 
@@ -1144,7 +829,6 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
         sl.stage.release(); sl.dig.release(); sl.dev.release();
         if (sl.done) (void)hipEventDestroy(sl.done);
     }
-    if (c->chain_stream) (void)hipStreamDestroy(c->chain_stream);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -1160,7 +844,7 @@ int mirsha_ctx_set_stream(mirsha_ctx* c, void* s) {
 void* mirsha_ctx_stream(mirsha_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
 
 int mirsha_ctx_set_variant(mirsha_ctx* c, int v) {
-    if (!c || v < mirsha::kVariantLds || v > mirsha::kVariantLdsOld) return MIRSHA_EINVAL;
+    if (!c || !mirsha::variant_valid(v)) return MIRSHA_EINVAL;
     c->variant = v;
     return MIRSHA_OK;
 }
@@ -1347,11 +1031,10 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
     }
     const uint64_t span = n_req ? hi - lo : 0;
     // Per-call plans cost host sorting and device allocations, so the host API
-    // uses a plan only when asked (MIRSHA_PIPELINE_MODE=fused|streams); the
+    // uses a plan only when asked (MIRSHA_PIPELINE_MODE=fused|auto); the
     // device API (mirsha_pipeline_create + *_device) amortises one plan.
     const char* pmode = getenv("MIRSHA_PIPELINE_MODE");
-    const bool pipelined = pmode && (strcmp(pmode, "fused") == 0 || strcmp(pmode, "streams") == 0 ||
-                                     strcmp(pmode, "auto") == 0 || strcmp(pmode, "cont") == 0);
+    const bool pipelined = pmode && (strcmp(pmode, "fused") == 0 || strcmp(pmode, "auto") == 0);
     if (pipelined && n_batches && n_req && span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES &&
         span <= 2 * total + 4096) {
         mirsha_pipeline p;
@@ -1403,7 +1086,8 @@ int mirsha_pipeline_create_mode(mirsha_ctx* c, uint32_t n_req, const uint32_t* l
                                 const uint32_t* list_first, uint32_t n_lists, int mode, mirsha_pipeline** out) {
     if (!c || !out) return MIRSHA_EINVAL;
     *out = nullptr;
-    if (mode < MIRSHA_PIPELINE_SEQUENTIAL || mode > MIRSHA_PIPELINE_CONT) return fail(c, MIRSHA_EINVAL, "bad mode %d", mode);
+    if (mode != MIRSHA_PIPELINE_SEQUENTIAL && mode != MIRSHA_PIPELINE_FUSED && mode != MIRSHA_PIPELINE_AUTO)
+        return fail(c, MIRSHA_EINVAL, "bad pipeline mode %d (sequential 0, fused 1, auto 3)", mode);
     if (int rc = check_lists(c, idx, list_first, n_lists, n_req)) return rc;
     if (int rc = use_device(c)) return rc;
     mirsha_pipeline* p = new mirsha_pipeline();
@@ -1431,11 +1115,10 @@ int mirsha_pipeline_mode(const mirsha_pipeline* p) { return p ? p->mode : MIRSHA
 int mirsha_pipeline_trace(mirsha_ctx* c, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words) {
     if (!c || !p || !words) return MIRSHA_EINVAL;
     *words = 0;
-    if ((p->mode != MIRSHA_PIPELINE_FUSED && p->mode != MIRSHA_PIPELINE_CONT) || !p->trace) return MIRSHA_OK;
+    if (p->mode != MIRSHA_PIPELINE_FUSED || !p->trace) return MIRSHA_OK;
     if (int rc = use_device(c)) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    const uint64_t n = p->mode == MIRSHA_PIPELINE_CONT ? 2ull * p->n_tiles + 2ull * p->n_counters
-                                                        : 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
+    const uint64_t n = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
     *words = n;
     if (out && cap) {
         HIP_TRY(c, hipMemcpyAsync(out, p->d_trace.p, 8ull * std::min(n, cap), hipMemcpyDeviceToHost, c->stream));
@@ -1456,14 +1139,6 @@ int mirsha_pipeline_status(mirsha_ctx* c, mirsha_pipeline* p) {
     if (!c || !p) return MIRSHA_EINVAL;
     if (int rc = use_device(c)) return rc;
     return fused_status(c, p);
-}
-
-int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap) {
-    if (!p || !n_segments) return MIRSHA_EINVAL;
-    *n_segments = (uint32_t)p->seg_bound.size();
-    if (bounds)
-        for (uint32_t i = 0; i < cap && i < p->seg_bound.size(); i++) bounds[i] = p->seg_bound[i];
-    return MIRSHA_OK;
 }
 
 int mirsha_hash_requests_then_batches_device(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena,
@@ -1673,6 +1348,46 @@ int mirsha_chains_reset(mirsha_ctx* c, mirsha_chains* ch, const uint32_t* which,
         }))
         return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return MIRSHA_OK;
+}
+
+int mirsha_clock_probe(mirsha_ctx* c, uint32_t iters, double* clock_ghz, double* cycles_per_wave_compression) {
+    if (!c || !clock_ghz || !cycles_per_wave_compression || iters == 0) return MIRSHA_EINVAL;
+    if (int rc = use_device(c)) return rc;
+    hipDeviceProp_t prop;
+    HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
+    // One 256-thread workgroup = one wave per SIMD of a CU; kProbeWavesPerSimd per CU.
+    const uint32_t blocks = (uint32_t)prop.multiProcessorCount * mirsha::kProbeWavesPerSimd;
+    const uint32_t waves = 4u * blocks;
+    DevBuf stamps, sink;
+    HIP_TRY(c, stamps.ensure(24ull * waves));
+    HIP_TRY(c, sink.ensure(4ull * 256u * blocks));
+    int rc = timed_launch(c, 2, [&] {
+        return mirsha::launch_clock_probe(blocks, iters, stamps.as<unsigned long long>(), sink.as<uint32_t>(),
+                                          c->stream);
+    });
+    std::vector<unsigned long long> h(3ull * waves);
+    if (rc == MIRSHA_OK) {
+        hipError_t e = hipMemcpyAsync(h.data(), stamps.p, 24ull * waves, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = fail(c, MIRSHA_EHIP, "clock probe: %s", hipGetErrorString(e));
+    }
+    stamps.release();
+    sink.release();
+    if (rc) return rc;
+    std::vector<double> ghz(waves);
+    unsigned long long first = ~0ull, last = 0;
+    for (uint32_t w = 0; w < waves; w++) {
+        const unsigned long long r0 = h[3 * w + 1], r1 = h[3 * w + 2];
+        ghz[w] = r1 > r0 ? 0.1 * (double)h[3 * w] / (double)(r1 - r0) : 0.0;
+        first = std::min(first, r0);
+        last = std::max(last, r1);
+    }
+    std::nth_element(ghz.begin(), ghz.begin() + waves / 2, ghz.end());
+    *clock_ghz = ghz[waves / 2];
+    // Span in shader cycles at that clock, per SIMD, per wave-compression.
+    const double span_cycles = (double)(last - first) * 10.0 * *clock_ghz;
+    *cycles_per_wave_compression = span_cycles / ((double)iters * mirsha::kProbeWavesPerSimd);
     return MIRSHA_OK;
 }
 

@@ -9,22 +9,21 @@ constexpr uint32_t kWavesPerBlock = 4;
 constexpr uint32_t kBlockThreads = 64 * kWavesPerBlock;
 constexpr uint32_t kNullIndex = 0xFFFFFFFFu;
 
-// sha256_msgs_kernel variants: loader (LDS-staged / direct per-lane loads) x
-// rounds (generated asm / compiler-scheduled C++).  Default: kVariantLds, whose
-// launches of at most kLowOccTiles tiles (<= 1 wave per SIMD) take the
-// low-occupancy kernel (prefetching direct loads, no-yield rounds).
-// kVariantLowOcc / kVariantLdsOnly force one of the two at any size (A/B, tests).
+// sha256_msgs_kernel forms.  Default kVariantLds: the LDS-staged coalesced
+// loader, whose small launches take latency forms (<= pair_max_groups()
+// tiles: producer/consumer pairs; <= kLowOccTiles tiles, one wave per SIMD:
+// the low-occupancy prefetching kernel).  The others force one form at any
+// size (A/B, tests).  Numbers 2, 3, 7, 8 (round-1 A/B forms) are retired.
 enum : int {
     kVariantLds = 0,
-    kVariantDirect = 1,
-    kVariantLdsCxx = 2,
-    kVariantDirectCxx = 3,
+    kVariantDirect = 1,   // direct per-lane loads
     kVariantLowOcc = 4,
     kVariantLdsOnly = 5,
     kVariantPair = 6,
-    kVariantLdsPf = 7,  // LDS loader, next block's loads in flight during the rounds
-    kVariantLdsOld = 8  // round-1 LDS loader (per-chunk activity and range tests)
 };
+inline bool variant_valid(int v) {
+    return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair;
+}
 constexpr uint32_t kLowOccTiles = 1024;   // 256 CUs x 4 SIMDs
 // Small launches take a latency form: at most pair_max_groups() 64-message
 // groups (default kPairMaxGroups: <= 2 pairs per CU, every wave alone on a
@@ -90,55 +89,6 @@ constexpr uint32_t kFusedTileYield = 2;  // issue-yield rounds in tile waves (pa
 // (kPacedLds of reserved LDS), `pace` tile waves per SIMD in tile blocks.
 constexpr uint32_t kPacedLds = 96u * 1024u;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
-// Continuation plan (MIRSHA_PIPELINE_CONT), see mirsha_kernels.hip: the
-// request launch at full occupancy; the tile wave that completes a list
-// group's segment counter hashes that segment itself (no waiting anywhere).
-// Lists are contiguous request ranges (list k = requests [cfirst[k],
-// cfirst[k+1])), segments cover ordinals [bound[s], bound[s+1]).
-constexpr uint32_t kContMaxSegments = 4;
-// Plan constants, in device memory (read only after a tile's own work, so
-// none of it stays live in registers across the request rounds).
-struct ContPlan {
-    const uint32_t* cfirst;      // n_lists + 1
-    const uint32_t* tadj_first;  // n_tiles + 1: counters each tile feeds
-    const uint32_t* tadj;
-    const uint32_t* ctarget;     // per counter (g * n_seg + s): feeding tiles + (s > 0)
-    unsigned long long* counters;
-    uint32_t* state;             // (n_seg - 1) x n_lists midstates, sc1 stores/loads
-    uint32_t n_lists, n_seg, flags, n_tiles;
-    uint32_t bound[kContMaxSegments];
-    uint32_t seg_tile[kContMaxSegments];  // first tile of each segment's requests (processing order)
-    uint32_t prio_tile;                   // kContSegPrioLate threshold (MIRSHA_CONT_PRIO_FRAC x n_tiles)
-    // Optional timeline (s_memrealtime, 100 MHz), NULL = off: per tile [start,
-    // end] at [2t, 2t+1], per counter c = g * n_seg + s its segment's [start,
-    // end] at [2 n_tiles + 2c, +1].
-    unsigned long long* trace;
-};
-struct ContArgs {
-    const uint8_t* arena;
-    uint64_t arena_len;
-    const uint64_t* off;
-    const uint32_t* len;
-    const uint32_t* order;       // n_req processing positions -> request
-    uint8_t* req_out;            // n_req digests, origin order (sc1 stores)
-    uint8_t* list_out;
-    const ContPlan* plan;        // device copy
-    uint32_t n_req, epoch, flags;  // flags: the plan's (kContSkipLists / kContPlainStores read here)
-};
-// MIRSHA_CONT_FLAGS (A/B knobs)
-constexpr uint32_t kContLatFinal = 1;  // no-yield rounds in final segments
-constexpr uint32_t kContNoPrio = 2;    // no issue priorities (default: tiles 1, segments 0)
-constexpr uint32_t kContSkipLists = 4;  // timing only: request tiles alone (list digests NOT computed)
-constexpr uint32_t kContPlainStores = 8;  // timing only: plain digest stores (no cross-CU visibility)
-constexpr uint32_t kContNoSegments = 16;  // timing only: counter adds, but no segment is hashed
-constexpr uint32_t kContLatAll = 32;     // no-yield rounds in every segment
-constexpr uint32_t kContSegNoLoads = 64;     // timing only: segments read no digests / state (wrong digests)
-constexpr uint32_t kContSegNoCompress = 128; // timing only: segments load but do not compress (wrong digests)
-constexpr uint32_t kContSegHighPrio = 256;   // segments 3, tiles 2 - the segment they feed (first design)
-constexpr uint32_t kContSegPrioTile = 512;   // segments at the tiles' priority (1)
-constexpr uint32_t kContSegPrioIndex = 1024; // segment s at priority min(s, 3)
-constexpr uint32_t kContSegPrioLate = 2048;  // segments run by tiles t >= prio_tile at priority 2, others 0
-hipError_t launch_cont(const ContArgs& a, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.
 hipError_t launch_chains_absorb(const uint8_t* digests, const uint32_t* pos, const uint32_t* act, const uint32_t* afirst,
@@ -151,5 +101,11 @@ hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, ui
 hipError_t launch_mixed_lengths(uint64_t seed, uint64_t first, uint64_t count, uint32_t* len, hipStream_t s);
 hipError_t launch_gen_mixed(uint64_t seed, uint64_t first, uint64_t count, const uint64_t* off, uint8_t* arena,
                             hipStream_t s);
+// Clock probe: `blocks` 256-thread workgroups of `iters` register-only
+// compressions each; stamps[3w] = shader cycles of wave w's loop, [3w+1],
+// [3w+2] = its start and end in 100 MHz ticks (s_memrealtime).
+constexpr uint32_t kProbeWavesPerSimd = 8;
+hipError_t launch_clock_probe(uint32_t blocks, uint32_t iters, unsigned long long* stamps, uint32_t* sink,
+                              hipStream_t s);
 
 }  // namespace mirsha

@@ -146,14 +146,6 @@ __device__ __forceinline__ void store_digest(uint8_t* out, uint32_t msg, const u
                       __builtin_bswap32(st[7]));
 }
 
-template <bool kAsm>
-__device__ __forceinline__ void compress_v(uint32_t st[8], uint32_t w[16]) {
-    if constexpr (kAsm)
-        compress_asm(st, w);
-    else
-        compress(st, w);
-}
-
 // Digest store with the sc1 cache policy: written through to memory (the line
 // leaves this XCD's L2), so a list wave on any XCD can read it with sc1 loads
 // once the storing wave has signalled (MI355X_MICROARCH.md, inter-workgroup
@@ -173,15 +165,13 @@ __device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uin
 
 // One wave hashes the tile of 64 messages at processing positions
 // [64 t, 64 t + 64) (order[] maps a position to a message; NULL = identity).
-// kSc1Out: digests are stored through `ors` with the sc1 policy (fused pass).
-// kPf (LDS loader only): block b+1's raw chunks are issued right after block
-// b's words leave LDS, so their loads are in flight during b's compression
-// (+20 VGPRs live across the rounds).
-template <bool kLds, bool kAsm, bool kSc1Out, bool kWide = false, bool kPf = false, bool kOld = false>
+// kLds: LDS-staged coalesced loader (else direct per-lane loads); kWide:
+// 64-bit per-lane addresses for arenas beyond one buffer descriptor.
+template <bool kLds, bool kWide>
 __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
-                                          __amdgpu_buffer_rsrc_t ors, uint4* my, uint32_t t, uint32_t lane) {
+                                          uint4* my, uint32_t t, uint32_t lane) {
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
@@ -206,106 +196,73 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] = kH0[i];
 
-    if constexpr (kLds) {
+    if constexpr (kLds && !kWide) {
         // Loader roles: this lane fetches quarter q of messages m_j = 16j + lane/4.
+        // Chunk addresses are loop-invariant VGPRs with the block in the
+        // scalar offset.  There is no per-chunk activity test: a finished
+        // message's chunk reads bytes nobody uses (in range) or zeros (out of
+        // range).  A tile whose every load stays in the arena (all but the
+        // arena's last tiles; a wave-uniform test) takes plain loads; the
+        // others range-check each chunk (the 5-dword tail form of
+        // issue_chunk).  The FIPS padding logic runs only on blocks that reach
+        // past the wave's shortest message.
         const uint32_t q = lane & 3u;
-        if constexpr (!kWide && !kPf && !kOld) {
-            // Chunk addresses are loop-invariant VGPRs with the block in the
-            // scalar offset.  There is no per-chunk activity test: a finished
-            // message's chunk reads bytes nobody uses (in range) or zeros (out
-            // of range).  A tile whose every load stays in the arena (all but
-            // the arena's last tiles; a wave-uniform test) takes plain
-            // loads; the others range-check each active-size chunk (the
-            // 5-dword tail form of issue_chunk).  The FIPS padding logic runs
-            // only on blocks that reach past the wave's shortest message.
-            const uint64_t reach = valid ? o + 64ull * wave_nb + 20u : 0ull;
-            const bool far = __builtin_amdgcn_ballot_w64(reach > records) == 0;
-            // Wave-uniform by construction; readfirstlane makes it an SGPR, so
-            // the padding test below is a scalar branch (as a VGPR compare it
-            // became an exec-mask branch with the word assembly duplicated).
-            const uint32_t min_l = __builtin_amdgcn_readfirstlane(wave_min(valid ? L : 0xFFFFFFFFu));
-            uint32_t vo[4], sel[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t a = (uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) + 16u * q;
-                vo[j] = a & ~3u;
-                sel[j] = be_sel(a & 3u);
-            }
-            for (uint32_t blk = 0; blk < wave_nb; blk++) {
-                const uint32_t soff = 64u * blk;
-                RawChunk rc[4];
-                if (far) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], soff, 0);
-                        rc[j].v[0] = v[0]; rc[j].v[1] = v[1]; rc[j].v[2] = v[2]; rc[j].v[3] = v[3];
-                        rc[j].v[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo[j], soff + 16u, 0);
-                    }
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) issue_chunk(rsrc, (uint32_t)records, vo[j] + soff, 0u, 0u, true, rc[j]);
-                }
-                const bool pad = soff + 64u > min_l;  // wave-uniform
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    uint32_t wq[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) wq[k] = be_word(rc[j].v[k + 1], rc[j].v[k], sel[j]);
-                    if (pad) {
-                        // Lengths fetched here (rare blocks), not kept live
-                        // across the rounds.
-                        const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(lane >> 2), 64);
-                        pad_words(soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
-                    }
-                    // Unconditional: a slot of a finished message is never read.
-                    my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
-                }
-                // Cross-lane hand-off inside one wave: LDS ops of a wave execute
-                // in order; the fences only stop the compiler from reordering.
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                uint32_t w[16];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint4 x = my[lds_slot(lane, (uint32_t)k)];
-                    w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (blk < nb) compress_v<kAsm>(st, w);
-            }
-        } else {
-        uint32_t Lj[4], nbj[4];
-        uint64_t oj[4];
+        const uint64_t reach = valid ? o + 64ull * wave_nb + 20u : 0ull;
+        const bool far = __builtin_amdgcn_ballot_w64(reach > records) == 0;
+        // Every message of the tile 4-byte aligned (wave-uniform): a chunk's
+        // words are its own 16 bytes, byte-swapped, so the fifth dword of the
+        // funnel shift is never loaded (4 instead of 8 loads per block).
+#ifdef MIRSHA_AB_NOALIGNED  // A/B build only (tools/ab_build.sh)
+        const bool aligned = false;
+#else
+        const bool aligned = __builtin_amdgcn_ballot_w64(valid && (o & 3u) != 0u) == 0;
+#endif
+        // Wave-uniform by construction; readfirstlane makes it an SGPR, so the
+        // padding test below is a scalar branch (as a VGPR compare it became
+        // an exec-mask branch with the word assembly duplicated).
+        const uint32_t min_l = __builtin_amdgcn_readfirstlane(wave_min(valid ? L : 0xFFFFFFFFu));
+        uint32_t vo[4], sel[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const int src = 16 * j + (int)(lane >> 2);
-            Lj[j] = (uint32_t)__shfl((int)L, src, 64);
-            oj[j] = (uint64_t)(uint32_t)__shfl((int)(uint32_t)o, src, 64);
-            if constexpr (kWide) oj[j] |= (uint64_t)(uint32_t)__shfl((int)(uint32_t)(o >> 32), src, 64) << 32;
-            nbj[j] = (uint32_t)__shfl((int)nb, src, 64);
-        }
-        RawChunk rc[4];
-        if constexpr (kPf) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) issue(oj[j], 0u, q, 0u < nbj[j], rc[j]);
+            const uint32_t a = (uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) + 16u * q;
+            vo[j] = a & ~3u;
+            sel[j] = be_sel(a & 3u);
         }
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
-            if constexpr (!kPf) {
+            const uint32_t soff = 64u * blk;
+            RawChunk rc[4];
+            if (far) {
 #pragma unroll
-                for (int j = 0; j < 4; j++) issue(oj[j], blk, q, blk < nbj[j], rc[j]);
+                for (int j = 0; j < 4; j++) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], soff, 0);
+                    rc[j].v[0] = v[0]; rc[j].v[1] = v[1]; rc[j].v[2] = v[2]; rc[j].v[3] = v[3];
+                    rc[j].v[4] = 0u;
+                }
+                if (!aligned) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        rc[j].v[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo[j], soff + 16u, 0);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; j++) issue_chunk(rsrc, (uint32_t)records, vo[j] + soff, 0u, 0u, true, rc[j]);
             }
+            const bool pad = soff + 64u > min_l;  // wave-uniform
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 uint32_t wq[4];
-                finish_chunk(rc[j], 64u * blk + 16u * q, Lj[j], blk + 1u == nbj[j], q, wq);
+#pragma unroll
+                for (int k = 0; k < 4; k++) wq[k] = be_word(rc[j].v[k + 1], rc[j].v[k], sel[j]);
+                if (pad) {
+                    // Lengths fetched here (rare blocks), not kept live across the rounds.
+                    const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(lane >> 2), 64);
+                    pad_words(soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
+                }
                 // Unconditional: a slot of a finished message is never read.
                 my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
             }
-            // Cross-lane hand-off inside one wave: LDS ops of a wave execute in
-            // order; the fences only stop the compiler from reordering them.
+            // Cross-lane hand-off inside one wave: LDS ops of a wave execute
+            // in order; the fences only stop the compiler from reordering.
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -318,14 +275,45 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if constexpr (kPf) {
-                if (blk + 1u < wave_nb) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) issue(oj[j], blk + 1u, q, blk + 1u < nbj[j], rc[j]);
-                }
-            }
-            if (blk < nb) compress_v<kAsm>(st, w);
+            if (blk < nb) compress_asm(st, w);
         }
+    } else if constexpr (kLds) {
+        // Wide arenas: the same LDS staging with per-chunk 64-bit addresses
+        // and activity tests (one launch over > 4 GiB, BASELINE config 5).
+        const uint32_t q = lane & 3u;
+        uint32_t Lj[4], nbj[4];
+        uint64_t oj[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int src = 16 * j + (int)(lane >> 2);
+            Lj[j] = (uint32_t)__shfl((int)L, src, 64);
+            oj[j] = (uint64_t)(uint32_t)__shfl((int)(uint32_t)o, src, 64);
+            oj[j] |= (uint64_t)(uint32_t)__shfl((int)(uint32_t)(o >> 32), src, 64) << 32;
+            nbj[j] = (uint32_t)__shfl((int)nb, src, 64);
+        }
+        for (uint32_t blk = 0; blk < wave_nb; blk++) {
+            RawChunk rc[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) issue(oj[j], blk, q, blk < nbj[j], rc[j]);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t wq[4];
+                finish_chunk(rc[j], 64u * blk + 16u * q, Lj[j], blk + 1u == nbj[j], q, wq);
+                my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+                w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (blk < nb) compress_asm(st, w);
         }
     } else {
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
@@ -337,18 +325,13 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
-            if (active) compress_v<kAsm>(st, w);
+            if (active) compress_asm(st, w);
         }
     }
-    if (valid) {
-        if constexpr (kSc1Out)
-            store_digest_sc1(ors, msg, st);
-        else
-            store_digest(out, msg, st);
-    }
+    if (valid) store_digest(out, msg, st);
 }
 
-template <bool kLds, bool kAsm, bool kWide = false, bool kPf = false, bool kOld = false>
+template <bool kLds, bool kWide = false>
 __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
@@ -358,9 +341,7 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * kWavesPerBlock + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<kLds, kAsm, false, kWide, kPf, kOld>(arena, arena_len, off, len, order, n, out,
-                                 __builtin_amdgcn_make_buffer_rsrc(nullptr, (short)0, 0, 0x00020000), tile[wv], t,
-                                 lane);
+    hash_tile<kLds, kWide>(arena, arena_len, off, len, order, n, out, tile[wv], t, lane);
 }
 
 // Low-occupancy form of the request kernel, for launches of at most one wave
@@ -1069,214 +1050,6 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     }
 }
 
-// ---- continuation plan: request launch + list segments, no waits -----------
-//
-// Many short lists (BatchSize 20, BASELINE config 2): a separate list launch
-// runs 820 lone chain waves of 11 compressions after the request kernel (37 us
-// of a 247 us step).  Here the request kernel keeps its full occupancy and
-// the list work rides on it: requests are processed in segment order (all
-// ordinals of segment 0 of every list first, then segment 1, ...), every tile
-// adds 1 to the counter of each (list group, segment) it feeds after its sc1
-// digest stores drained, and the wave whose add COMPLETES a counter hashes
-// that segment of the group's 64 lists (lane = list) at once, then adds 1 to
-// the next segment's counter (which also waits for its own tiles); whoever
-// completes that one continues.  Nobody waits, so there is no deadlock and
-// no watchdog.  Segments of early groups interleave with later request tiles
-// at full occupancy; only the last segments (<= 2 digest blocks + padding)
-// trail the launch.
-//
-// Visibility: digests and midstates are stored sc1 (written through, dropped
-// from the writer's L2) and read sc1 by the completing wave after the
-// counter said every producer's stores drained.  The plan admits a shape only
-// if no 128-B line of request digests is shared by two (group, segment)
-// pairs (contiguous lists, BatchSize and segment bounds multiples of 4,
-// 128-B aligned output), so no L2 can hold a line before it is complete.
-// Midstates: one region per segment, each line written once and read once per
-// run.
-template <bool kLat>
-__device__ __forceinline__ void cont_segment(const ContPlan& a, uint8_t* list_out, __amdgpu_buffer_rsrc_t drs,
-                                             __amdgpu_buffer_rsrc_t srs, uint32_t g, uint32_t s, uint32_t lane) {
-    const uint32_t k = g * 64u + lane;
-    const bool valid = k < a.n_lists;
-    const uint32_t e0 = valid ? a.cfirst[k] : 0u;  // first request of the list (contiguous lists)
-    const uint32_t c = valid ? a.cfirst[k + 1] - e0 : 0u;
-    const uint32_t ob = a.bound[s];
-    const uint32_t oe = s + 1u < a.n_seg ? a.bound[s + 1u] : kOpenEnd;
-    const bool active = valid && (ob == 0u || c > ob);
-    const bool fin = active && c <= oe;
-    const uint32_t full_end = fin ? (c & ~1u) : oe;  // exclusive ordinal of the full blocks
-    const uint32_t nblk = active ? (full_end - ob) / 2u + (fin ? 1u : 0u) : 0u;
-    const uint32_t wave_nb = wave_max(nblk);
-    const uint32_t L = 32u * c;
-    uint32_t st[8];
-    if (ob == 0u) {
-#pragma unroll
-        for (int i = 0; i < 8; i++) st[i] = kH0[i];
-    } else {
-        const uint32_t so = 32u * ((s - 1u) * a.n_lists + k);
-        const bool ld = active && !(a.flags & kContSegNoLoads);
-        const auto x0 = __builtin_amdgcn_raw_buffer_load_b128(srs, ld ? so : 0xFFFFFFE0u, 0, kSc1);
-        const auto x1 = __builtin_amdgcn_raw_buffer_load_b128(srs, ld ? so + 16u : 0xFFFFFFE0u, 0, kSc1);
-        st[0] = x0[0]; st[1] = x0[1]; st[2] = x0[2]; st[3] = x0[3];
-        st[4] = x1[0]; st[5] = x1[1]; st[6] = x1[2]; st[7] = x1[3];
-    }
-    for (uint32_t t = 0; t < wave_nb; t++) {
-        const uint32_t d0 = ob + 2u * t;
-        uint4 x[4];
-        const bool ld = !(a.flags & kContSegNoLoads);
-        load_digest_sc1(drs, e0 + d0, ld && t < nblk && d0 < c, x[0], x[1]);
-        load_digest_sc1(drs, e0 + d0 + 1u, ld && t < nblk && d0 + 1u < c, x[2], x[3]);
-        uint32_t w[16];
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-            const uint32_t di = d0 + (uint32_t)half;
-            const uint4 x0 = x[2 * half], x1 = x[2 * half + 1];
-            // Past the end the loads returned zeros; only the 0x80 marker is added.
-            w[8 * half + 0] = __builtin_bswap32(x0.x) | (fin && di == c ? 0x80000000u : 0u);
-            w[8 * half + 1] = __builtin_bswap32(x0.y); w[8 * half + 2] = __builtin_bswap32(x0.z);
-            w[8 * half + 3] = __builtin_bswap32(x0.w); w[8 * half + 4] = __builtin_bswap32(x1.x);
-            w[8 * half + 5] = __builtin_bswap32(x1.y); w[8 * half + 6] = __builtin_bswap32(x1.z);
-            w[8 * half + 7] = __builtin_bswap32(x1.w);
-        }
-        if (fin && t + 1u == nblk) {
-            w[14] = L >> 29;
-            w[15] = L << 3;
-        }
-        if (t < nblk && !(a.flags & kContSegNoCompress)) {
-            if constexpr (kLat)
-                compress_asm_lat(st, w);
-            else
-                compress_asm(st, w);
-        } else if (t < nblk) {
-#pragma unroll
-            for (int i = 0; i < 8; i++) st[i] ^= w[i] ^ w[i + 8];  // keep the loads live
-        }
-    }
-    if (fin) {
-        store_digest(list_out, k, st);
-    } else if (active) {
-        const uint32_t so = 32u * (s * a.n_lists + k);
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        __builtin_amdgcn_raw_buffer_store_b128((v4u){st[0], st[1], st[2], st[3]}, srs, so, 0, kSc1);
-        __builtin_amdgcn_raw_buffer_store_b128((v4u){st[4], st[5], st[6], st[7]}, srs, so + 16u, 0, kSc1);
-    }
-}
-
-// Runs segment `ctr` (wave-uniform counter id, just completed) and every later
-// segment of the same group whose counter this wave then completes.
-__device__ __forceinline__ void cont_chain(const ContPlan& a, uint8_t* list_out, uint32_t epoch, __amdgpu_buffer_rsrc_t drs,
-                                          __amdgpu_buffer_rsrc_t srs, uint32_t ctr, uint32_t lane, uint32_t t) {
-    if (a.flags & kContSegPrioLate) {
-        if (t >= a.prio_tile)
-            __builtin_amdgcn_s_setprio(2);
-        else
-            __builtin_amdgcn_s_setprio(0);
-    }
-    while (true) {
-        const uint32_t g = ctr / a.n_seg, s = ctr - g * a.n_seg;
-        const bool last = s + 1u == a.n_seg;
-        asm volatile("" ::: "memory");  // no load of the segment above the completing add
-        if (a.flags & kContSegPrioTile) {
-            __builtin_amdgcn_s_setprio(1);
-        } else if (a.flags & kContSegPrioIndex) {
-            if (s == 0)
-                __builtin_amdgcn_s_setprio(0);
-            else if (s == 1)
-                __builtin_amdgcn_s_setprio(1);
-            else if (s == 2)
-                __builtin_amdgcn_s_setprio(2);
-            else
-                __builtin_amdgcn_s_setprio(3);
-        }
-        if (a.trace && lane == 0) a.trace[2ull * a.n_tiles + 2ull * ctr] = __builtin_amdgcn_s_memrealtime();
-        if ((last && (a.flags & kContLatFinal)) || (a.flags & kContLatAll))
-            cont_segment<true>(a, list_out, drs, srs, g, s, lane);
-        else
-            cont_segment<false>(a, list_out, drs, srs, g, s, lane);
-        if (a.trace) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) a.trace[2ull * a.n_tiles + 2ull * ctr + 1u] = __builtin_amdgcn_s_memrealtime();
-        }
-        if (last) return;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // midstate stores drained before the signal
-        uint32_t go = 0;
-        if (lane == 0) {
-            const unsigned long long old =
-                __hip_atomic_fetch_add(a.counters + ctr + 1u, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            go = old + 1ull == (unsigned long long)epoch * a.ctarget[ctr + 1u];
-        }
-        if (!__shfl((int)go, 0, 64)) return;
-        ctr++;
-    }
-}
-
-// Register budget left to hipcc (78 VGPRs, 6 waves per SIMD, no scratch):
-// forcing 8 waves per SIMD spilled 11 VGPRs to scratch and measured slower
-// with segments (0.346 vs 0.333 ms), equal without them (0.211 vs 0.210 ms).
-// One wave per workgroup: a wave that goes on to hash list segments must not
-// hold a finished workgroup's LDS and slots (4-wave workgroups: 0.397 ms per
-// config-2 launch, 1-wave: 0.332 ms).  Issue priorities: tiles 1, segments 0,
-// so a segment wave only fills the tiles' issue bubbles (0.277 ms; segments at
-// 3 and tiles by the segment they feed, the first design: 0.333 ms).
-__global__ __launch_bounds__(64) void sha256_msgs_cont_kernel(ContArgs ca) {
-    __shared__ uint4 tile[256];
-    const uint32_t t = blockIdx.x;
-    if (t * 64u >= ca.n_req) return;
-    {
-        const ContPlan& p = *ca.plan;
-        if (!(p.flags & (kContSegHighPrio | kContNoPrio))) {
-            __builtin_amdgcn_s_setprio(1);
-        } else if (p.flags & kContSegHighPrio) {
-            const uint32_t ph = (p.n_seg > 1u && t >= p.seg_tile[1]) + (p.n_seg > 2u && t >= p.seg_tile[2]);
-            if (ph == 0)
-                __builtin_amdgcn_s_setprio(2);
-            else if (ph == 1)
-                __builtin_amdgcn_s_setprio(1);
-        }
-    }
-    const __amdgpu_buffer_rsrc_t drs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)ca.req_out, (short)0, (int)(32u * ca.n_req), 0x00020000);
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    if (ca.flags & kContPlainStores)
-        hash_tile<true, true, false>(ca.arena, ca.arena_len, ca.off, ca.len, ca.order, ca.n_req, ca.req_out, drs, tile,
-                                     t, threadIdx.x & 63u);
-    else
-        hash_tile<true, true, true>(ca.arena, ca.arena_len, ca.off, ca.len, ca.order, ca.n_req, nullptr, drs, tile, t,
-                                    threadIdx.x & 63u);
-    if (ca.flags & kContSkipLists) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's digest stores drained before its adds
-    // Recomputed rather than kept live across the rounds (VGPR budget of 8 waves per SIMD).
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const ContPlan& p = *ca.plan;
-    if (p.trace && (threadIdx.x & 63u) == 0) {
-        p.trace[2ull * t] = t_start;
-        p.trace[2ull * t + 1u] = __builtin_amdgcn_s_memrealtime();
-    }
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)p.state, (short)0, (int)(32u * (p.n_seg - 1u) * p.n_lists), 0x00020000);
-    const uint32_t j0 = p.tadj_first[t], j1 = p.tadj_first[t + 1];
-    for (uint32_t j = j0; j < j1; j += 64u) {
-        const bool mine = j + lane < j1;
-        const uint32_t ctr = mine ? p.tadj[j + lane] : 0u;
-        bool done = false;
-        if (mine) {
-            const unsigned long long old =
-                __hip_atomic_fetch_add(p.counters + ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            done = old + 1ull == (unsigned long long)ca.epoch * p.ctarget[ctr] && !(ca.flags & kContNoSegments);
-        }
-        uint64_t m = __builtin_amdgcn_ballot_w64(done);
-        if (m && !(p.flags & (kContSegHighPrio | kContNoPrio)))
-            __builtin_amdgcn_s_setprio(0);
-        else if (m && (p.flags & kContSegHighPrio))
-            __builtin_amdgcn_s_setprio(3);
-        while (m) {
-            const int l = __builtin_ctzll(m);
-            m &= m - 1u;
-            cont_chain(p, ca.list_out, ca.epoch, drs, srs, (uint32_t)__shfl((int)ctr, l, 64), lane, t);
-        }
-    }
-}
-
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1344,6 +1117,42 @@ __global__ void gen_mixed_kernel(uint64_t seed, uint64_t first, uint64_t count, 
     }
 }
 
+// ---- clock probe (bench diagnostics; no digest depends on it) ---------------
+// Every SIMD runs kProbeWavesPerSimd waves of back-to-back throughput-form
+// compressions on registers (the request kernel's rounds, no memory traffic);
+// lane 0 of each wave records the shader-clock cycles (s_memtime) of its loop
+// and the 100 MHz reference time (s_memrealtime) at its start and end.  Cycles
+// over ticks is the clock the chip holds under this VALU load
+// (MI355X_MICROARCH.md, DVFS item 6); the launch span (first start to last
+// end) x clock / (iters x waves per SIMD) is the SIMD cost of one
+// wave-compression: the achievable ceiling of the request kernel.
+__global__ __launch_bounds__(256) void clock_probe_kernel(uint32_t iters, unsigned long long* __restrict__ stamps,
+                                                          uint32_t* __restrict__ sink) {
+    uint32_t st[8], w[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i] ^ threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 16; i++) w[i] = kK[i] + blockIdx.x;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t b = 0; b < iters; b++) compress_asm(st, w);  // w keeps W[48..63]: fresh input
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63u) == 0u) {
+        stamps[3ull * gw] = t1 - t0;
+        stamps[3ull * gw + 1ull] = r0;
+        stamps[3ull * gw + 2ull] = r1;
+    }
+    sink[blockIdx.x * 256u + threadIdx.x] = st[0] ^ st[7];
+}
+
+hipError_t launch_clock_probe(uint32_t blocks, uint32_t iters, unsigned long long* stamps, uint32_t* sink,
+                              hipStream_t s) {
+    clock_probe_kernel<<<blocks, 256, 0, s>>>(iters, stamps, sink);
+    return hipGetLastError();
+}
+
 // ---- host-side launchers --------------------------------------------------
 uint32_t pair_max_groups() {
     static const uint32_t v = [] {
@@ -1361,8 +1170,8 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
     if (n == 0) return hipSuccess;
     const uint32_t tiles = (n + 63u) / 64u;
     const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
-    if (arena_len > kMaxBufferArena) {  // 64-bit per-lane addressing (LDS loader, asm rounds)
-        sha256_msgs_kernel<true, true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+    if (arena_len > kMaxBufferArena) {  // 64-bit per-lane addressing (LDS loader)
+        sha256_msgs_kernel<true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantPair || (variant == kVariantLds && tiles <= pair_max_groups())) {
@@ -1373,38 +1182,10 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
-    // MIRSHA_MSGS_OCC=k (A/B): cap the waves per SIMD at k by reserving LDS
-    // (each 4-wave workgroup takes 1/k of the CU's 160 KiB).
-    static const size_t occ_lds = [] {
-        const char* e = getenv("MIRSHA_MSGS_OCC");
-        const uint32_t k = e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
-        const size_t stat = sizeof(uint4) * kWavesPerBlock * 256u;
-        return (k >= 1 && k <= 8) ? (size_t)(160u * 1024u / k) - stat : (size_t)0;
-    }();
-    switch (variant) {
-        case kVariantLds:
-        case kVariantLdsOnly:
-            sha256_msgs_kernel<true, true><<<grid, kBlockThreads, occ_lds, s>>>(arena, arena_len, off, len, order, n,
-                                                                               out);
-            break;
-        case kVariantLdsPf:
-            sha256_msgs_kernel<true, true, false, true><<<grid, kBlockThreads, occ_lds, s>>>(arena, arena_len, off, len,
-                                                                                          order, n, out);
-            break;
-        case kVariantLdsOld:
-            sha256_msgs_kernel<true, true, false, false, true><<<grid, kBlockThreads, occ_lds, s>>>(
-                arena, arena_len, off, len, order, n, out);
-            break;
-        case kVariantDirect:
-            sha256_msgs_kernel<false, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
-            break;
-        case kVariantLdsCxx:
-            sha256_msgs_kernel<true, false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
-            break;
-        default:
-            sha256_msgs_kernel<false, false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
-            break;
-    }
+    if (variant == kVariantDirect)
+        sha256_msgs_kernel<false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+    else
+        sha256_msgs_kernel<true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
     return hipGetLastError();
 }
 
@@ -1446,13 +1227,6 @@ hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, 
         attr = true;
     }
     sha256_fused_paced_kernel<<<grid, 256u * pace, kPacedLds, s>>>(a);
-    return hipGetLastError();
-}
-
-hipError_t launch_cont(const ContArgs& a, hipStream_t s) {
-    if (a.n_req == 0) return hipSuccess;
-    if (!a.plan || a.arena_len > kMaxBufferArena) return hipErrorInvalidValue;
-    sha256_msgs_cont_kernel<<<(a.n_req + 63u) / 64u, 64, 0, s>>>(a);
     return hipGetLastError();
 }
 

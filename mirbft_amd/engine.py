@@ -20,25 +20,18 @@ KERNEL_LISTS = 1
 KERNEL_GEN = 2
 KERNEL_CHAIN = 3
 KERNEL_FUSED = 4
-KERNEL_CONT = 5
 
 # mirsha_pipeline modes (include/mirsha.h)
 PIPELINE_SEQUENTIAL = 0
 PIPELINE_FUSED = 1
-PIPELINE_STREAMS = 2
 PIPELINE_AUTO = 3
-PIPELINE_CONT = 4
-PIPELINE_MODES = {"sequential": PIPELINE_SEQUENTIAL, "fused": PIPELINE_FUSED, "streams": PIPELINE_STREAMS,
-                  "auto": PIPELINE_AUTO, "cont": PIPELINE_CONT}
+PIPELINE_MODES = {"sequential": PIPELINE_SEQUENTIAL, "fused": PIPELINE_FUSED, "auto": PIPELINE_AUTO}
 VARIANT_LDS = 0
 VARIANT_DIRECT = 1
-VARIANT_LDS_CXX = 2
-VARIANT_DIRECT_CXX = 3
 VARIANT_LOWOCC = 4
 VARIANT_LDS_ONLY = 5
 VARIANT_PAIR = 6
-VARIANT_LDS_PF = 7
-VARIANT_LDS_OLD = 8
+VARIANTS = (VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR)
 
 
 def _ptr(a: np.ndarray | None) -> int | None:
@@ -326,7 +319,7 @@ class Engine:
 
     def pipeline(self, n_req: int, idx, list_first, length=None, mode: int | str | None = None) -> "Pipeline":
         """Plan for request -> batch-digest runs with this list shape (host index lists).
-        mode: PIPELINE_AUTO (default) / _FUSED / _SEQUENTIAL / _STREAMS or its name."""
+        mode: PIPELINE_AUTO (default) / _FUSED / _SEQUENTIAL or its name."""
         return Pipeline(self, n_req, idx, list_first, length, mode)
 
     def hash_requests_then_batches_device(self, plan: "Pipeline", d_arena: int, arena_len: int, d_off: int,
@@ -344,6 +337,13 @@ class Engine:
     def synth_mixed_device(self, seed: int, first: int, count: int, d_off: int, d_arena: int) -> None:
         """Config-5 message bytes of requests [first, first + count) at d_arena + d_off[r]."""
         self._check(self._lib.mirsha_synth_mixed_device(self.ctx, seed, first, count, d_off, d_arena))
+
+    def clock_probe(self, iters: int = 128) -> tuple[float, float]:
+        """(clock GHz held under the compression load, SIMD cycles per 64-lane
+        compression with no memory traffic): mirsha_clock_probe."""
+        ghz, cyc = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        self._check(self._lib.mirsha_clock_probe(self.ctx, int(iters), ctypes.byref(ghz), ctypes.byref(cyc)))
+        return ghz.value, cyc.value
 
 
 class Pipeline:
@@ -393,13 +393,6 @@ class Pipeline:
         self._engine._check(self._lib.mirsha_pipeline_trace(self._engine.ctx, self.handle, _ptr(out), n.value,
                                                             ctypes.byref(n)))
         return out
-
-    def segments(self) -> list[int]:
-        n = ctypes.c_uint32(0)
-        check(self._lib.mirsha_pipeline_segments(self.handle, ctypes.byref(n), None, 0))
-        b = np.zeros(max(n.value, 1), dtype=np.uint32)
-        check(self._lib.mirsha_pipeline_segments(self.handle, ctypes.byref(n), _ptr(b), n.value))
-        return b[: n.value].tolist()
 
     def close(self) -> None:
         if getattr(self, "handle", None):
@@ -500,16 +493,13 @@ __all__ = [
     "KERNEL_GEN",
     "KERNEL_CHAIN",
     "KERNEL_FUSED",
-    "KERNEL_CONT",
     "PIPELINE_SEQUENTIAL",
     "PIPELINE_FUSED",
-    "PIPELINE_STREAMS",
     "PIPELINE_AUTO",
     "VARIANT_LDS",
     "VARIANT_DIRECT",
     "VARIANT_LOWOCC",
     "VARIANT_LDS_ONLY",
     "VARIANT_PAIR",
-    "VARIANT_LDS_PF",
-    "VARIANT_LDS_OLD",
+    "VARIANTS",
 ]

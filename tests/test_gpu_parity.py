@@ -14,18 +14,16 @@ import synth
 from mirbft_amd import (ActionResults, Actions, Engine, HashRequest, MirshaError, Processor, ProcessorWorkPool,
                         gpu_hasher, hash_batch_multi, hashdata, sharding)
 from mirbft_amd import _lib
-from mirbft_amd.engine import (KERNEL_LISTS, KERNEL_MSGS, VARIANT_DIRECT, VARIANT_DIRECT_CXX, VARIANT_LDS,
-                               VARIANT_LDS_CXX, VARIANT_LDS_OLD, VARIANT_LDS_ONLY, VARIANT_LDS_PF, VARIANT_LOWOCC,
-                               VARIANT_PAIR)
+from mirbft_amd.engine import (KERNEL_LISTS, KERNEL_MSGS, VARIANT_DIRECT, VARIANT_LDS, VARIANT_LDS_ONLY,
+                               VARIANT_LOWOCC, VARIANT_PAIR)
 
 pytestmark = pytest.mark.gpu
 
 EMPTY = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 
 
-@pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LDS_CXX, VARIANT_DIRECT_CXX, VARIANT_LOWOCC,
-                        VARIANT_LDS_ONLY, VARIANT_PAIR, VARIANT_LDS_PF, VARIANT_LDS_OLD],
-                ids=["lds", "direct", "lds_cxx", "direct_cxx", "lowocc", "lds_only", "pair", "lds_pf", "lds_old"])
+@pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR],
+                ids=["lds", "direct", "lowocc", "lds_only", "pair"])
 def eng(engine, request):
     engine.set_variant(request.param)
     yield engine
@@ -454,30 +452,6 @@ def test_pipeline_device_full_size(engine, mode, cfg, data_len, n, bs):
     plan.close()
 
 
-def test_pipeline_streams_mode(engine):
-    """The two-stream segment split (MIRSHA_PIPELINE_STREAMS) stays bit-exact."""
-    torch = _torch()
-    n, data_len, bs = 40000, 256, 20
-    stride = 16 + data_len
-    idx, first = sharding.batch_lists(n, bs)
-    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="streams")
-    assert len(plan.segments()) > 1
-    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
-    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
-    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
-    d_req = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
-    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
-    engine.synth_requests_device(5, 0, n, data_len, d_arena.data_ptr())
-    engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
-                                             d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
-    engine.sync()
-    want_req = oracle_py.hash_requests(oracle_py.gen_requests(5, 0, n, data_len),
-                                       np.arange(n, dtype=np.uint64) * stride, np.full(n, stride))
-    assert np.array_equal(d_req.cpu().numpy(), want_req)
-    assert np.array_equal(d_bat.cpu().numpy(), oracle_py.batch_digests(want_req, idx, first))
-    plan.close()
-
-
 def _irregular(seed, n=3000, n_lists=300, max_list=60, max_len=600):
     rng = np.random.default_rng(seed)
     lens = rng.integers(0, max_len, n).astype(np.uint32)
@@ -492,7 +466,7 @@ def _irregular(seed, n=3000, n_lists=300, max_list=60, max_len=600):
     return arena, off, lens, idx, first
 
 
-@pytest.mark.parametrize("env_mode", [None, "fused", "streams", "auto", "sequential"])
+@pytest.mark.parametrize("env_mode", [None, "fused", "auto", "sequential"])
 def test_pipeline_irregular_lists(engine, monkeypatch, env_mode):
     """Shared requests, unlisted requests, nulls, empty and odd lists through the
     host API (general path, or a per-call plan when MIRSHA_PIPELINE_MODE is set)."""
@@ -594,100 +568,25 @@ def _contiguous(seed, n, bs, listed, max_len):
     return arena, off, lens, idx, first
 
 
-@pytest.mark.parametrize("seed,n,bs,listed,max_len,bounds", [
-    (51, 40010, 20, 40010, 300, None),   # BatchSize 20: segments [0,8) [8,16) [16,20); ragged last batch of 10
-    (52, 5003, 8, 5003, 200, None),      # BatchSize 8: [0,4) [4,8); last batch of 3
-    (53, 3001, 12, 2900, 500, None),     # unlisted requests after the lists (processed last, no counter)
-    (54, 70000, 500, 70000, 120, None),  # VerifyBatch-sized lists: [0,248) [248,496) [496,500)
-    (55, 64 * 20 * 3 + 1, 20, 64 * 20 * 3 + 1, 100, None),  # last group = one list of one request
-    (56, 20000, 20, 20000, 300, "4,8,12"),  # 4 segments (MIRSHA_CONT_BOUNDS)
-    (57, 20000, 20, 20000, 300, "16"),      # 2 segments
-])
-def test_cont_plan(engine, monkeypatch, seed, n, bs, listed, max_len, bounds):
-    """Continuation plan (one launch; the request wave completing a batch
-    segment hashes it): bit-exact request and batch digests, three runs on one
-    plan (epoch-scaled counter targets)."""
-    if bounds:
-        monkeypatch.setenv("MIRSHA_CONT_BOUNDS", bounds)
-    arena, off, lens, idx, first = _contiguous(seed, n, bs, listed, max_len)
-    plan = engine.pipeline(n, idx, first, lens, mode="cont")
-    assert plan.mode_name == "cont"
-    if bounds:
-        assert list(plan.segments()) == [0] + [int(x) for x in bounds.split(",")]
-    want_req = oracle_py.hash_requests(arena, off, lens, threads=8)
-    want_lst = oracle_py.batch_digests(want_req, idx, first)
-    for req, lst in _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=3):
-        assert np.array_equal(req, want_req)
-        assert np.array_equal(lst, want_lst)
-    plan.close()
+@pytest.mark.parametrize("variant", [2, 3, 7, 8, 9, -1])
+def test_retired_variants_rejected(engine, variant):
+    """Round-1 A/B kernel forms are out of the product: EINVAL, not a silent default."""
+    with pytest.raises(MirshaError) as e:
+        engine.set_variant(variant)
+    assert e.value.code == _lib.MIRSHA_EINVAL
 
 
-@pytest.mark.parametrize("shape", ["odd_batch", "not_contiguous", "nulls"])
-def test_cont_plan_falls_back(engine, shape):
-    """Shapes the continuation plan does not admit run as the two-kernel plan."""
-    n = 3000
-    arena, off, lens, idx, first = _contiguous(61, n, 20, n, 200)
-    if shape == "odd_batch":
-        idx, first = sharding.batch_lists(n, 7)
-    elif shape == "not_contiguous":
-        idx = idx[::-1].copy()
-    else:
-        idx = idx.copy()
-        idx[5] = _lib.MIRSHA_NULL_INDEX
-    plan = engine.pipeline(n, idx, first, lens, mode="cont")
-    assert plan.mode_name == "sequential"
-    want_req = oracle_py.hash_requests(arena, off, lens)
-    for req, lst in _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=1):
-        assert np.array_equal(req, want_req)
-        assert np.array_equal(lst, oracle_py.batch_digests(want_req, idx, first))
-    plan.close()
+@pytest.mark.parametrize("mode", [2, 4, 5])
+def test_retired_pipeline_modes_rejected(engine, mode):
+    idx, first = sharding.batch_lists(64, 20)
+    with pytest.raises(MirshaError) as e:
+        engine.pipeline(64, idx, first, np.full(64, 272), mode=mode)
+    assert e.value.code == _lib.MIRSHA_EINVAL
 
 
-def test_cont_plan_misaligned_output(engine):
-    """Digests not 128-B aligned: the plan runs its two-kernel fallback."""
-    torch = _torch()
-    n, bs = 9000, 20
-    arena, off, lens, idx, first = _contiguous(62, n, bs, n, 300)
-    plan = engine.pipeline(n, idx, first, lens, mode="cont")
-    d_arena = torch.from_numpy(arena).cuda()
-    d_off = torch.from_numpy(off.view(np.int64)).cuda()
-    d_len = torch.from_numpy(lens.view(np.int32)).cuda()
-    d_req = torch.zeros((n + 1, 32), dtype=torch.uint8, device="cuda")
-    d_lst = torch.zeros((first.size - 1, 32), dtype=torch.uint8, device="cuda")
-    engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), arena.size, d_off.data_ptr(),
-                                             d_len.data_ptr(), d_req[1:].data_ptr(), d_lst.data_ptr())
-    plan.status()
-    want_req = oracle_py.hash_requests(arena, off, lens)
-    assert np.array_equal(d_req[1:].cpu().numpy(), want_req)
-    assert np.array_equal(d_lst.cpu().numpy(), oracle_py.batch_digests(want_req, idx, first))
-    plan.close()
-
-
-def test_cont_plan_full_size_config2(engine):
-    """BASELINE config 2 (2^20 x 256-B requests, BatchSize 20) through the
-    continuation plan, twice, bit-exact vs the oracle."""
-    torch = _torch()
-    n, data_len, bs = 1 << 20, 256, 20
-    stride = 16 + data_len
-    seed = synth.SEED_BASE + 2
-    idx, first = sharding.batch_lists(n, bs)
-    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="cont")
-    assert plan.mode_name == "cont"
-    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
-    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
-    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
-    d_req = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
-    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
-    engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
-    want_req = oracle_py.hash_requests(oracle_py.gen_requests(seed, 0, n, data_len),
-                                       np.arange(n, dtype=np.uint64) * stride, np.full(n, stride), threads=8)
-    want_bat = oracle_py.batch_digests(want_req, idx, first)
-    for _ in range(2):
-        d_req.zero_()
-        d_bat.zero_()
-        engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
-                                                 d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
-        plan.status()
-        assert np.array_equal(d_req.cpu().numpy(), want_req)
-        assert np.array_equal(d_bat.cpu().numpy(), want_bat)
-    plan.close()
+def test_clock_probe_sane(engine):
+    """The bench's clock probe: a clock within the part's range and a
+    compression cost no cheaper than the spec issue floor (2 x 1,384 cycles)."""
+    ghz, cyc = engine.clock_probe(8)
+    assert 0.5 < ghz < 3.0
+    assert 2 * 1384 <= cyc < 50000

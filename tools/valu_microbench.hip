@@ -162,6 +162,7 @@ void run(const char* name, int blocks, unsigned* d_out, unsigned long long* d_cl
 }
 
 #include "../mirbft_amd/csrc/sha256_device.h"
+#include "sha256_rounds_asm_ab.h"
 
 // Pure-register SHA-256 compression loop (generated-asm rounds): the
 // achievable per-compression cost with no memory traffic at all.
