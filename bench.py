@@ -288,7 +288,10 @@ class BatchWorkload:
 
     def cpu_baseline(self, seconds):
         """Oracle (C port of processor.go:133-143 with SHA-NI compression, the
-        instruction class Go's crypto/sha256 uses on amd64) on the host cores."""
+        instruction class Go's crypto/sha256 uses on amd64) on the host cores:
+        the serial Processor on one core (the headline), and the order-
+        preserving ProcessorWorkPool analogue with HashWorkers = NumCPU() (the
+        reference default, processor.go:406-408) and with the cgroup quota."""
         o = _oracle()
         stride, bs = self.stride, self.bs
         n = min(self.n, 1 << 16)
@@ -302,20 +305,44 @@ class BatchWorkload:
             d = o.hash_requests(arena, off, ln, threads=threads)
             o.batch_digests(d, idx, first)
 
-        res = _time_cpu(one, seconds, (1, pool_threads()))
+        res = _time_cpu(one, seconds, (1,))
         per = n + first.size - 1
         done1, dt1 = res[1]
-        tp = max(res)
+        facts = _cpu_facts()
+        # Pool legs on a larger sample (whole config up to 2^20 requests), so
+        # per-pass thread start-up is noise; batch digests single-threaded, as
+        # the state machine consumes them (processResults, state_machine.go:377-433).
+        npool = min(self.n, 1 << 20)
+        npool -= npool % bs
+        parena = o.gen_requests(self.seed, 0, npool, self.data_len)
+        poff = np.arange(npool, dtype=np.uint64) * stride
+        pln = np.full(npool, stride, dtype=np.uint32)
+        pidx, pfirst = sharding.batch_lists(npool, bs)
+        pper = npool + pfirst.size - 1
+        legs = {}
+        for name, t in (("numcpu", facts["affinity_cpus"] or 1),
+                        ("quota", int(facts["cgroup_cpu_quota"] or 0))):
+            if t < 2 or t in [v["threads"] for v in legs.values()]:
+                continue
+
+            def pool(threads):
+                d = o.hash_requests(parena, poff, pln, threads=threads)
+                o.batch_digests(d, pidx, pfirst)
+
+            r = _time_cpu(pool, seconds / 3, (t,))[t]
+            legs[name] = {"value": r[0] * pper / r[1], "threads": t,
+                          "sample": f"{r[0]} passes x {npool} requests + {pfirst.size - 1} batch digests, {r[1]:.1f} s"}
         return {
             "value": done1 * per / dt1, "unit": "digests/s", "cores": 1, "kind": "port",
             "sample": f"{done1} passes x ({n} requests x {stride} B + {first.size - 1} BatchSize-{bs} batch "
                       f"digests), {dt1:.1f} s, oracle C port of processor.go:133-143 (serial Processor), "
                       f"SHA-NI compression (stand-in for Go crypto/sha256 amd64 asm)",
-            "pool": {"value": res[tp][0] * per / res[tp][1], "threads": tp,
-                     "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361), "
-                             "HashWorkers = runtime.NumCPU() = the affinity mask (processor.go:406-408)"},
+            "pool": {**legs,
+                     "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361): workers pull "
+                             "requests from a shared counter; numcpu = HashWorkers = runtime.NumCPU() = the affinity "
+                             "mask (processor.go:406-408), quota = the container's CPU quota"},
             "cpu": _cpu_model(),
-            **_cpu_facts(),
+            **facts,
         }
 
     def config_fields(self):

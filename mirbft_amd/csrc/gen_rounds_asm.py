@@ -267,10 +267,10 @@ AB_VARIANTS = {
 }
 
 
-def emit_fn(name, ch_mode, add_mode, k_mode, nops):
+def emit_fn(name, ch_mode, add_mode, k_mode, nops, rounds=(0, 64)):
     out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16]) {{",
            "    uint32_t t0, t1, t2, t3;" + (" uint32_t kt;" if k_mode == "smov" else "")]
-    for j0 in range(0, 64, 8):
+    for j0 in range(rounds[0], rounds[1], 8):
         body = block(j0, ch_mode, add_mode, k_mode, nops)
         out.append(f"    // rounds {j0}..{j0 + 7}")
         out.append("    asm volatile(")
@@ -311,6 +311,10 @@ def emit():
     ]
     for name, (ch, ad, km, nops) in VARIANTS.items():
         out += emit_fn(name, ch, ad, km, nops)
+    out.append("// rounds_asm in two halves (rounds 0..31, 32..63), for a loader that issues")
+    out.append("// the next block's loads between them.")
+    out += emit_fn("rounds_asm_lo", *VARIANTS["rounds_asm"], rounds=(0, 32))
+    out += emit_fn("rounds_asm_hi", *VARIANTS["rounds_asm"], rounds=(32, 64))
     out.append("// 8 consumer rounds with K + W precomputed (pair kernels): names rotate")
     out.append("// back after 8 rounds, so the same statement serves every 8-round chunk.")
     out += emit_fn_kw("rounds_kw8_asm")

@@ -24,23 +24,37 @@
 
 namespace mirsha {
 
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64);
-        v = v < o ? v : o;
-    }
-    return v;
+// Wave-wide max / min, wave-uniform result (an SGPR).  DPP inside each 16-lane
+// row (quad_perm xor 1 / xor 2, row_ror 4 / 8: four VALU ops, no LDS), then
+// the four row results by v_readlane and a scalar reduction.  Called with all
+// 64 lanes active (every call site is at a kernel's top, before divergence);
+// a DPP source outside the row keeps the lane's own value.
+template <bool kMax>
+__device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
+    auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : (a < b ? a : b); };
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    return op(op(r0, r1), op(r2, r3));
 }
-
+#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 shuffle reductions
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64);
-        v = v > o ? v : o;
-    }
-    return v;
+    for (int s = 1; s < 64; s <<= 1) { const uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64); v = v > o ? v : o; }
+    return __builtin_amdgcn_readfirstlane(v);
 }
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) { const uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64); v = v < o ? v : o; }
+    return __builtin_amdgcn_readfirstlane(v);
+}
+#else
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) { return wave_reduce<true>(v); }
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) { return wave_reduce<false>(v); }
+#endif
 
 // Raw 20 bytes (5 dwords) covering the 16-byte chunk q of block blk of a
 // message at arena offset o: aligned down to 4 bytes, the byte shift is
@@ -163,6 +177,24 @@ __device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uin
         ors, 32u * msg + 16u, 0, kSc1);
 }
 
+#ifdef MIRSHA_AB_STAMPS
+// Diagnostic build only (tools/ab_build.sh stamps): per request tile, the
+// 100 MHz time at wave start / metadata ready / first block landed / end,
+// and the wave's HW_ID and XCC_ID, for tools/stamp_run.py.  No output
+// depends on them.
+constexpr uint32_t kStampWords = 6, kStampTiles = 1u << 16;
+__device__ unsigned long long g_stamps[kStampWords * kStampTiles];
+#define MIRSHA_STAMP(t, i)                                                               \
+    do {                                                                                 \
+        const unsigned long long _v = __builtin_amdgcn_s_memrealtime();                 \
+        if (lane == 0u && (t) < kStampTiles) g_stamps[kStampWords * (t) + (i)] = _v;      \
+    } while (0)
+#else
+#define MIRSHA_STAMP(t, i) \
+    do {                   \
+    } while (0)
+#endif
+
 // One wave hashes the tile of 64 messages at processing positions
 // [64 t, 64 t + 64) (order[] maps a position to a message; NULL = identity).
 // kLds: LDS-staged coalesced loader (else direct per-lane loads); kWide:
@@ -171,14 +203,35 @@ template <bool kLds, bool kWide>
 __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
-                                          uint4* my, uint32_t t, uint32_t lane) {
+                                          uint4* my, uint32_t* my_extra, uint32_t t, uint32_t lane) {
+    MIRSHA_STAMP(t, 0);
+    // Prologue at the highest issue priority: a freshly started wave is the
+    // youngest on its SIMD and, at the default priority, gets the VALU only
+    // when every older wave stalls -- its metadata loads, reductions and first
+    // DMA then took ~20 us of a ~60 us wave life (tools/stamp_run.py), which
+    // left only ~3 of 8 resident waves computing.  Back to 0 at the first
+    // compression.
+#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 prologue (default priority, conditional loads)
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
     const uint32_t L = valid ? len[msg] : 0u;
     const uint64_t o = valid ? off[msg] : 0u;
+#else
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t slot = t * 64u + lane;
+    const bool valid = slot < n;
+    // Unconditional loads (n >= 1; an idle lane reads the last message's
+    // entries), so the length and offset loads issue together.
+    const uint32_t slot_c = valid ? slot : n - 1u;
+    const uint32_t msg = order ? order[slot_c] : slot_c;
+    const uint32_t L_ = len[msg];
+    const uint64_t o_ = off[msg];
+    const uint32_t L = valid ? L_ : 0u;
+    const uint64_t o = valid ? o_ : 0u;
+#endif
     const uint32_t nb = valid ? blocks_for_len(L) : 0u;
-    const uint32_t wave_nb = wave_max(nb);
+    const uint32_t wave_nb = wave_max(nb);  // wave-uniform (SGPR): scalar block-loop tests
 
     // Bytes past arena_len inside the last dword are never part of a message
     // (they are masked by the padding logic), so the range rounds up to 4.
@@ -217,10 +270,101 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #else
         const bool aligned = __builtin_amdgcn_ballot_w64(valid && (o & 3u) != 0u) == 0;
 #endif
-        // Wave-uniform by construction; readfirstlane makes it an SGPR, so the
-        // padding test below is a scalar branch (as a VGPR compare it became
-        // an exec-mask branch with the word assembly duplicated).
-        const uint32_t min_l = __builtin_amdgcn_readfirstlane(wave_min(valid ? L : 0xFFFFFFFFu));
+        // Wave-uniform (SGPR), so the padding test below is a scalar branch (as
+        // a VGPR compare it became an exec-mask branch with the word assembly
+        // duplicated).
+        const uint32_t min_l = wave_min(valid ? L : 0xFFFFFFFFu);
+#ifndef MIRSHA_AB_REGLOADER  // A/B build only (tools/ab_build.sh): round-1 register-staged loader everywhere
+        if (far) {
+            // LDS-DMA loader: each block's 64 x 64 B go global -> LDS directly
+            // (buffer_load ... lds, no VGPR staging, no ds_write), issued one
+            // block AHEAD: block b+1's DMA starts as soon as the wave has read
+            // block b's words, so it lands during block b's compression.
+            // DMA lane roles: instruction j writes 1 KiB at my + 64 j, lane L's
+            // 16 B at slot 64 j + L = 4 m + (L & 3) for message m = 16 j + L / 4;
+            // that slot must hold quarter (L & 3) ^ ((m >> 2) & 3) (the XOR
+            // swizzle of lds_slot), and (m >> 2) & 3 = (L >> 4) & 3 for every j.
+            // Each message's 4 quarters are still fetched by 4 adjacent lanes
+            // (64 contiguous bytes).  A misaligned tile also DMAs the dword
+            // after each message's block window (the funnel's 17th dword) into
+            // my_extra[m], one dword per lane.
+            const uint32_t qd = (lane & 3u) ^ ((lane >> 4) & 3u);
+            uint32_t va[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                va[j] = ((uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) & ~3u) + 16u * qd;
+            const uint32_t ve = ((uint32_t)o & ~3u) + 64u;  // own message: dword after block 0's window
+            const uint32_t own_sel = be_sel((uint32_t)o & 3u);
+            typedef __attribute__((address_space(3))) void* lds_ptr_t;
+            auto dma = [&](uint32_t soff) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(my + 64 * j), 16, va[j], soff, 0, 0);
+                if (!aligned) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)my_extra, 4, ve, soff, 0, 0);
+            };
+            MIRSHA_STAMP(t, 1);
+            dma(0u);
+            for (uint32_t blk = 0; blk < wave_nb; blk++) {
+                const uint32_t soff = 64u * blk;
+                // This wave's DMA of block blk has landed (LDS-DMA counts in vmcnt).
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                if (blk == 0u) MIRSHA_STAMP(t, 2);
+                uint32_t raw[17];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+                    raw[4 * k + 0] = x.x; raw[4 * k + 1] = x.y; raw[4 * k + 2] = x.z; raw[4 * k + 3] = x.w;
+                }
+                raw[16] = aligned ? 0u : my_extra[lane];
+                // The reads completed before the next DMA overwrites the tile.
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#ifdef MIRSHA_AB_DMA_EARLY  // A/B build only: next block's DMA before this block's rounds
+                if (blk + 1u < wave_nb) dma(soff + 64u);
+#endif
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) w[k] = be_word(raw[k + 1], raw[k], own_sel);
+                if (soff + 64u > min_l) {  // wave-uniform: a block past the wave's shortest message
+                    const bool last = blk + 1u == nb;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) pad_words(soff + 16u * k, L, last, (uint32_t)k, &w[4 * k]);
+                }
+                if (blk == 0u) __builtin_amdgcn_s_setprio(0);
+                // Rounds on every lane (a lane past its message discards the
+                // result), so the DMA between the halves runs with all lanes:
+                // its lane roles are loader roles, not this lane's message.
+                // Issued half a compression ahead: enough to cover the load,
+                // and half the bytes in flight of a whole-block lead, which
+                // keeps the memory queues (and every other load) shorter.
+                uint32_t s8[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) s8[i] = st[i];
+                rounds_asm_lo(s8, w);
+#ifndef MIRSHA_AB_DMA_EARLY
+                if (blk + 1u < wave_nb) dma(soff + 64u);
+#endif
+                rounds_asm_hi(s8, w);
+                if (blk < nb) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) st[i] += s8[i];
+                }
+            }
+            MIRSHA_STAMP(t, 3);
+#ifdef MIRSHA_AB_STAMPS
+            {
+                unsigned hw, xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                if (lane == 0u && t < kStampTiles) {
+                    g_stamps[kStampWords * t + 4] = hw;
+                    g_stamps[kStampWords * t + 5] = xcc;
+                }
+            }
+#endif
+            if (valid) store_digest(out, msg, st);
+            return;
+        }
+#endif
         uint32_t vo[4], sel[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -275,6 +419,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (blk == 0u) __builtin_amdgcn_s_setprio(0);
             if (blk < nb) compress_asm(st, w);
         }
     } else if constexpr (kLds) {
@@ -313,6 +458,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (blk == 0u) __builtin_amdgcn_s_setprio(0);
             if (blk < nb) compress_asm(st, w);
         }
     } else {
@@ -325,23 +471,35 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
+            if (blk == 0u) __builtin_amdgcn_s_setprio(0);
             if (active) compress_asm(st, w);
         }
     }
     if (valid) store_digest(out, msg, st);
 }
 
+// One wave per workgroup: a workgroup's slot and LDS are released only when
+// ALL its waves have finished, and the SIMD arbiter's age order finishes a
+// workgroup's waves (one per SIMD) far apart, so 4-wave workgroups left SIMDs
+// below their 8-wave occupancy (tools/stamp_run.py).  8 waves per SIMD bound
+// the register budget to 64 VGPRs (the wide form keeps 6: 80 VGPRs, no spill).
+#ifdef MIRSHA_AB_WG4  // A/B build only (tools/ab_build.sh): 4-wave workgroups
+constexpr uint32_t kMsgWaves = 4;
+#else
+constexpr uint32_t kMsgWaves = 1;
+#endif
 template <bool kLds, bool kWide = false>
-__global__ __launch_bounds__(kBlockThreads) void sha256_msgs_kernel(
+__global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : 8) void sha256_msgs_kernel(
     const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
     uint8_t* __restrict__ out) {
-    __shared__ uint4 tile[kWavesPerBlock][256];
+    __shared__ uint4 tile[kMsgWaves][256];
+    __shared__ uint32_t extra[kMsgWaves][64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t t = blockIdx.x * kWavesPerBlock + wv;
+    const uint32_t t = blockIdx.x * kMsgWaves + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<kLds, kWide>(arena, arena_len, off, len, order, n, out, tile[wv], t, lane);
+    hash_tile<kLds, kWide>(arena, arena_len, off, len, order, n, out, tile[wv], extra[wv], t, lane);
 }
 
 // Low-occupancy form of the request kernel, for launches of at most one wave
@@ -1147,6 +1305,13 @@ __global__ __launch_bounds__(256) void clock_probe_kernel(uint32_t iters, unsign
     sink[blockIdx.x * 256u + threadIdx.x] = st[0] ^ st[7];
 }
 
+#ifdef MIRSHA_AB_STAMPS
+extern "C" int mirsha_ab_stamps(unsigned long long* out, uint64_t words) {
+    if (words > (uint64_t)kStampWords * kStampTiles) words = (uint64_t)kStampWords * kStampTiles;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 8 * words, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif
+
 hipError_t launch_clock_probe(uint32_t blocks, uint32_t iters, unsigned long long* stamps, uint32_t* sink,
                               hipStream_t s) {
     clock_probe_kernel<<<blocks, 256, 0, s>>>(iters, stamps, sink);
@@ -1170,8 +1335,9 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
     if (n == 0) return hipSuccess;
     const uint32_t tiles = (n + 63u) / 64u;
     const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
+    const uint32_t mgrid = (tiles + kMsgWaves - 1u) / kMsgWaves;
     if (arena_len > kMaxBufferArena) {  // 64-bit per-lane addressing (LDS loader)
-        sha256_msgs_kernel<true, true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        sha256_msgs_kernel<true, true><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantPair || (variant == kVariantLds && tiles <= pair_max_groups())) {
@@ -1183,9 +1349,9 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         return hipGetLastError();
     }
     if (variant == kVariantDirect)
-        sha256_msgs_kernel<false><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        sha256_msgs_kernel<false><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
     else
-        sha256_msgs_kernel<true><<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        sha256_msgs_kernel<true><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
     return hipGetLastError();
 }
 
@@ -1292,7 +1458,9 @@ __global__ __launch_bounds__(kBlockThreads) void chains_absorb_kernel(
 #pragma unroll
             for (int i = 0; i < 8; i++) w[i] = pw[i];
         } else {
-            load_digest_words(digests, pos[e0 + (uint32_t)q], live, w);
+            // Guarded like the second load below: past this lane's own block
+            // count the index would run beyond its range in pos.
+            load_digest_words(digests, live ? pos[e0 + (uint32_t)q] : 0u, live, w);
         }
         load_digest_words(digests, live ? pos[e0 + (uint32_t)(q + 1)] : 0u, live, w + 8);
         if (live) compress_asm_lat(st, w);

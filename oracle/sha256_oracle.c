@@ -14,6 +14,7 @@
 #include "oracle.h"
 
 #include <pthread.h>
+#include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -213,20 +214,31 @@ typedef struct {
     const uint64_t* off;
     const uint32_t* len;
     uint8_t* out;
-    uint32_t begin, end;
+    uint32_t n;
+    _Atomic uint32_t* next;  /* shared work counter: ProcessorWorkPool's channel hand-off */
 } mt_job;
+
+enum { kMtChunk = 256 };
 
 static void* mt_worker(void* arg) {
     mt_job* j = (mt_job*)arg;
     oracle_sha256 h;
-    for (uint32_t i = j->begin; i < j->end; i++) {
-        oracle_sha256_reset(&h);  /* serviceHashPool reuses one hasher with Reset, :313,:325 */
-        oracle_sha256_write(&h, j->arena + j->off[i], j->len[i]);
-        oracle_sha256_sum(&h, j->out + 32 * (size_t)i);
+    for (;;) {
+        const uint32_t b = atomic_fetch_add(j->next, kMtChunk);
+        if (b >= j->n) break;
+        const uint32_t e = b + kMtChunk < j->n ? b + kMtChunk : j->n;
+        for (uint32_t i = b; i < e; i++) {
+            oracle_sha256_reset(&h);  /* serviceHashPool reuses one hasher with Reset, :313,:325 */
+            oracle_sha256_write(&h, j->arena + j->off[i], j->len[i]);
+            oracle_sha256_sum(&h, j->out + 32 * (size_t)i);
+        }
     }
     return NULL;
 }
 
+/* The ProcessorWorkPool analogue (processor.go:312-361): `threads` workers pull
+ * requests from a shared counter (dynamic, like the reference's channel), each
+ * writing digests at the request's own index (origin order kept). */
 void oracle_hash_requests_mt(const uint8_t* arena, const uint64_t* off, const uint32_t* len,
                              uint32_t n, uint8_t* out, int threads) {
     if (threads <= 1 || n < 2) {
@@ -234,17 +246,12 @@ void oracle_hash_requests_mt(const uint8_t* arena, const uint64_t* off, const ui
         return;
     }
     if ((uint32_t)threads > n) threads = (int)n;
+    _Atomic uint32_t next = 0;
     pthread_t* tid = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)threads);
-    mt_job* jobs = (mt_job*)malloc(sizeof(mt_job) * (size_t)threads);
-    for (int t = 0; t < threads; t++) {
-        jobs[t].arena = arena; jobs[t].off = off; jobs[t].len = len; jobs[t].out = out;
-        jobs[t].begin = (uint32_t)((uint64_t)n * t / threads);
-        jobs[t].end = (uint32_t)((uint64_t)n * (t + 1) / threads);
-        pthread_create(&tid[t], NULL, mt_worker, &jobs[t]);
-    }
+    mt_job job = {arena, off, len, out, n, &next};
+    for (int t = 0; t < threads; t++) pthread_create(&tid[t], NULL, mt_worker, &job);
     for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
     free(tid);
-    free(jobs);
 }
 
 /* sequence.go:154-157: data[i] = ack.Digest; null requests carry an empty

@@ -66,3 +66,23 @@ def test_invalid_chain_ids_raise(engine):
     with pytest.raises(MirshaError):
         ch.reset([4])
     ch.close()
+
+
+def test_uneven_absorb_one_long_one_short_chain(engine):
+    """One chain gets ~1e5 digests in one call, the highest chain id gets 1
+    (a short chain stored after a long one in the same wave must not
+    read its index list past its own end), plus odd pending counts."""
+    n = 64
+    ch = CheckpointChains(engine, n)
+    ref = [hashlib.sha256() for _ in range(n)]
+    rng = np.random.default_rng(11)
+    for m_long in (100_001, 3):
+        digests = rng.integers(0, 256, (m_long + 1, 32), dtype=np.uint8)
+        chain_of = np.zeros(m_long + 1, dtype=np.uint32)
+        chain_of[-1] = n - 1
+        ch.write(digests, chain_of)
+        for d, c in zip(digests, chain_of):
+            ref[c].update(d.tobytes())
+    every = np.arange(n, dtype=np.uint32)
+    assert [g.tobytes() for g in ch.sum(every)] == [r.digest() for r in ref]
+    ch.close()

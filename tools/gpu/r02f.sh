@@ -1,0 +1,18 @@
+#!/bin/bash
+# r02f: tests, timeline with the high-priority prologue + DPP reductions, A/B.
+set -uo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r02f; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
+rc=$?; tail -3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit 1
+MIRSHA_AB_LIB=tools/scratch/stamps/libmirsha.so timeout -k 10 180 python -u tools/stamp_run.py $O/stamps > $O/stamps.json 2> $O/stamps.err || { tail -20 $O/stamps.err; exit 1; }
+cat $O/stamps.json
+for r in 1 2 3; do
+  for lib in product regloader dmaearly; do
+    L=""; [ $lib = product ] || L=tools/scratch/$lib/libmirsha.so
+    MIRSHA_AB_LIB=$L timeout -k 10 120 python -u bench.py --steps 50 --warmup 5 --cpu-seconds 0 --no-pcie > $O/ab_${lib}_$r.jsonl 2>> $O/ab.err || exit 1
+  done
+  echo ab rep $r done
+done
+timeout -k 10 240 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.jsonl 2> $O/bench_driver.err || exit 1
+echo all done
