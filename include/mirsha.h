@@ -167,6 +167,21 @@ int mirsha_submit_slices(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
 int mirsha_wait(mirsha_ctx* ctx, uint64_t ticket);
 int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
 
+/* Host-side phases (milliseconds) of the context's last slice submission
+ * (mirsha_submit_slices / mirsha_hash_slices_dedup): validate = slice
+ * lengths; plan = dedup plan (fingerprint + byte-for-byte confirm); pack =
+ * gather into pinned staging + bucket order; device = queued -> complete (H2D,
+ * kernel, D2H, plus any time the caller spent before waiting); scatter =
+ * digests copied to the caller in origin order.  Writes min(n, phases)
+ * entries; returns the number of phases. */
+#define MIRSHA_PROF_VALIDATE 0
+#define MIRSHA_PROF_PLAN 1
+#define MIRSHA_PROF_PACK 2
+#define MIRSHA_PROF_DEVICE 3
+#define MIRSHA_PROF_SCATTER 4
+#define MIRSHA_PROF_PHASES 5
+int mirsha_ctx_host_profile(const mirsha_ctx* ctx, double* ms_out, int n);
+
 /* Request digests, then the dependent batch digests computed ON DEVICE from
  * the device-resident request digests (no host round trip):
  *   batch b = SHA-256(concat(req_digest[idx[e]] for e in [batch_first[b], batch_first[b+1])))

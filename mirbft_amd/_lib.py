@@ -99,6 +99,7 @@ SIGNATURES = {
     "mirsha_synth_mixed_lengths_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p]),
     "mirsha_synth_mixed_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p]),
     "mirsha_clock_probe": (c_int, [c_void_p, c_uint32, POINTER(c_double), POINTER(c_double)]),
+    "mirsha_ctx_host_profile": (c_int, [c_void_p, POINTER(c_double), c_int]),
 }
 
 

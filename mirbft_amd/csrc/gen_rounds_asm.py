@@ -311,10 +311,6 @@ def emit():
     ]
     for name, (ch, ad, km, nops) in VARIANTS.items():
         out += emit_fn(name, ch, ad, km, nops)
-    out.append("// rounds_asm in two halves (rounds 0..31, 32..63), for a loader that issues")
-    out.append("// the next block's loads between them.")
-    out += emit_fn("rounds_asm_lo", *VARIANTS["rounds_asm"], rounds=(0, 32))
-    out += emit_fn("rounds_asm_hi", *VARIANTS["rounds_asm"], rounds=(32, 64))
     out.append("// 8 consumer rounds with K + W precomputed (pair kernels): names rotate")
     out.append("// back after 8 rounds, so the same statement serves every 8-round chunk.")
     out += emit_fn_kw("rounds_kw8_asm")

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -72,8 +73,14 @@ struct PinnedBuf {
 // its own pinned staging and device buffers, so up to kAsyncSlots Ready()
 // cycles can be packed / copied / hashed while the caller works on.
 constexpr uint32_t kAsyncSlots = 4;
+using Clock = std::chrono::steady_clock;
+inline double ms_since(Clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
 struct AsyncSlot {
     PinnedBuf stage;  // [arena bytes | off u64[m] | len u32[m] | order u32[m]]
+    Clock::time_point t_queued;  // when its device work was queued
     PinnedBuf dig;    // m x 32 digests (D2H target)
     DevBuf dev;       // the same layout as stage, then m x 32 digests
     hipEvent_t done = nullptr;
@@ -107,6 +114,7 @@ struct mirsha_ctx {
     AsyncSlot slots[kAsyncSlots];
     uint64_t next_ticket = 1;  // ticket of the next submission
     uint64_t done_ticket = 0;  // every ticket <= this one has completed
+    double prof[MIRSHA_PROF_PHASES] = {};  // host phases of the last slice submission (ms)
 };
 
 // Streaming checkpoint chains (see mirsha.h, mirsha_chains_create).
@@ -128,7 +136,7 @@ struct mirsha_pipeline {
     uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
     uint32_t fused_flags = 0;                             // mirsha::kFusedTile* (MIRSHA_FUSED_FLAGS)
     uint64_t tile_base = 0, list_base = 0;
-    uint32_t epoch = 0;
+    uint64_t epoch = 0;  // completed runs of a fused plan
     DevBuf d_tadj_first, d_tadj, d_cbase, d_expected, d_counters, d_ctl, d_trace;
     bool trace = false;
     std::vector<uint32_t> cidx, cfirst;      // compacted lists (no null entries)
@@ -562,7 +570,7 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.n_req = p->n_req;
     a.n_entries = p->n_entries;
     a.n_lists = p->n_lists;
-    a.epoch = p->epoch + 1u;
+    a.epoch = p->epoch + 1ull;
     a.n_tiles = p->n_tiles;
     a.n_groups = p->n_groups;
     a.list_waves = p->list_blocks;
@@ -671,6 +679,8 @@ int slice_lengths(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t
 // Copies a completed submission's digests to the caller, in origin order.
 int async_complete(mirsha_ctx* c, AsyncSlot& sl) {
     HIP_TRY(c, hipEventSynchronize(sl.done));
+    const auto t_done = Clock::now();
+    c->prof[MIRSHA_PROF_DEVICE] = std::chrono::duration<double, std::milli>(t_done - sl.t_queued).count();
     const uint8_t* d = sl.dig.as<uint8_t>();
     if (sl.rank.empty()) {
         memcpy(sl.user_out, d, 32ull * sl.n);
@@ -679,6 +689,7 @@ int async_complete(mirsha_ctx* c, AsyncSlot& sl) {
     }
     sl.busy = false;
     c->done_ticket = std::max(c->done_ticket, sl.ticket);
+    c->prof[MIRSHA_PROF_SCATTER] = ms_since(t_done);
     return MIRSHA_OK;
 }
 
@@ -697,10 +708,14 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
                  const uint32_t* slice_first, uint32_t n, uint8_t* out, int flags, uint64_t* ticket_out,
                  uint32_t* n_unique_out) {
     if (flags & ~MIRSHA_SUBMIT_DEDUP) return fail(c, MIRSHA_EINVAL, "unknown submit flags 0x%x", flags);
+    auto t0 = Clock::now();
+    for (double& x : c->prof) x = 0.0;
     std::vector<uint32_t> len;
     if (n) {
         if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     }
+    c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
+    t0 = Clock::now();
     if (int rc = use_device(c)) return rc;
     AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
     if (sl.busy)
@@ -727,6 +742,8 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
         }
     }
     if (n_unique_out) *n_unique_out = m;
+    c->prof[MIRSHA_PROF_PLAN] = ms_since(t0);
+    t0 = Clock::now();
     std::vector<uint64_t> poff(m);
     std::vector<uint32_t> plen(m);
     uint64_t bytes = 0;
@@ -752,6 +769,8 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     memcpy(st + o_off, poff.data(), 8ull * m);
     memcpy(st + o_len, plen.data(), 4ull * m);
     const bool identity = bucket_order(plen.data(), m, reinterpret_cast<uint32_t*>(st + o_ord));
+    c->prof[MIRSHA_PROF_PACK] = ms_since(t0);
+    sl.t_queued = Clock::now();
     uint8_t* dv = sl.dev.as<uint8_t>();
     if (m) {
         HIP_TRY(c, hipMemcpyAsync(dv, st, o_end, hipMemcpyHostToDevice, c->stream));
@@ -1349,6 +1368,12 @@ int mirsha_chains_reset(mirsha_ctx* c, mirsha_chains* ch, const uint32_t* which,
         return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return MIRSHA_OK;
+}
+
+int mirsha_ctx_host_profile(const mirsha_ctx* c, double* ms_out, int n) {
+    if (!c || !ms_out || n < 0) return MIRSHA_EINVAL;
+    for (int k = 0; k < n && k < MIRSHA_PROF_PHASES; k++) ms_out[k] = c->prof[k];
+    return MIRSHA_PROF_PHASES;
 }
 
 int mirsha_clock_probe(mirsha_ctx* c, uint32_t iters, double* clock_ghz, double* cycles_per_wave_compression) {

@@ -80,7 +80,10 @@ struct FusedArgs {
     uint32_t n_counters;
     unsigned long long tile_base, list_base;
     uint32_t arena_len, n_req, n_entries, n_lists;
-    uint32_t epoch, n_tiles, n_groups, list_waves;
+    // Run number of the plan (1, 2, ...): counters are monotone over runs and a
+    // chunk is ready at epoch x expected; 64-bit so it never wraps.
+    unsigned long long epoch;
+    uint32_t n_tiles, n_groups, list_waves;
     uint32_t flags;  // kFusedTilePrio | kFusedTileYield (A/B knobs, MIRSHA_FUSED_FLAGS)
 };
 constexpr uint32_t kFusedTilePrio = 1;   // s_setprio 2/1/0 for tiles by ticket third (early tiles first)

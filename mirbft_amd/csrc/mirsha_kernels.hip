@@ -178,8 +178,9 @@ __device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uin
 }
 
 #ifdef MIRSHA_AB_STAMPS
-// Diagnostic build only (tools/ab_build.sh stamps): per request tile, the
-// 100 MHz time at wave start / metadata ready / first block landed / end,
+// Diagnostic build only (tools/ab_build.sh stamps): per request tile of the
+// LDS loader, the 100 MHz time at wave start / metadata ready / first block
+// staged / end,
 // and the wave's HW_ID and XCC_ID, for tools/stamp_run.py.  No output
 // depends on them.
 constexpr uint32_t kStampWords = 6, kStampTiles = 1u << 16;
@@ -189,9 +190,23 @@ __device__ unsigned long long g_stamps[kStampWords * kStampTiles];
         const unsigned long long _v = __builtin_amdgcn_s_memrealtime();                 \
         if (lane == 0u && (t) < kStampTiles) g_stamps[kStampWords * (t) + (i)] = _v;      \
     } while (0)
+#define MIRSHA_STAMP_END(t)                                                              \
+    do {                                                                                 \
+        MIRSHA_STAMP(t, 3);                                                              \
+        unsigned _hw, _xcc;                                                              \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_hw));                \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_xcc));              \
+        if (lane == 0u && (t) < kStampTiles) {                                           \
+            g_stamps[kStampWords * (t) + 4] = _hw;                                       \
+            g_stamps[kStampWords * (t) + 5] = _xcc;                                      \
+        }                                                                                \
+    } while (0)
 #else
 #define MIRSHA_STAMP(t, i) \
     do {                   \
+    } while (0)
+#define MIRSHA_STAMP_END(t) \
+    do {                    \
     } while (0)
 #endif
 
@@ -203,22 +218,22 @@ template <bool kLds, bool kWide>
 __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
-                                          uint4* my, uint32_t* my_extra, uint32_t t, uint32_t lane) {
+                                          uint4* my, uint32_t t, uint32_t lane) {
     MIRSHA_STAMP(t, 0);
-    // Prologue at the highest issue priority: a freshly started wave is the
-    // youngest on its SIMD and, at the default priority, gets the VALU only
-    // when every older wave stalls -- its metadata loads, reductions and first
-    // DMA then took ~20 us of a ~60 us wave life (tools/stamp_run.py), which
-    // left only ~3 of 8 resident waves computing.  Back to 0 at the first
-    // compression.
-#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 prologue (default priority, conditional loads)
+    // The prologue stays at the default issue priority: a fresh wave is the
+    // youngest on its SIMD and issues when older ones stall.  Raising it
+    // (s_setprio 3 until the first compression) got the new waves computing
+    // sooner but measured 1 % slower (profiles/r02g).
+#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 prologue (conditional loads)
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
     const uint32_t L = valid ? len[msg] : 0u;
     const uint64_t o = valid ? off[msg] : 0u;
 #else
+#ifdef MIRSHA_AB_PRIO  // A/B build only: high-priority prologue
     __builtin_amdgcn_s_setprio(3);
+#endif
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     // Unconditional loads (n >= 1; an idle lane reads the last message's
@@ -274,97 +289,6 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         // a VGPR compare it became an exec-mask branch with the word assembly
         // duplicated).
         const uint32_t min_l = wave_min(valid ? L : 0xFFFFFFFFu);
-#ifndef MIRSHA_AB_REGLOADER  // A/B build only (tools/ab_build.sh): round-1 register-staged loader everywhere
-        if (far) {
-            // LDS-DMA loader: each block's 64 x 64 B go global -> LDS directly
-            // (buffer_load ... lds, no VGPR staging, no ds_write), issued one
-            // block AHEAD: block b+1's DMA starts as soon as the wave has read
-            // block b's words, so it lands during block b's compression.
-            // DMA lane roles: instruction j writes 1 KiB at my + 64 j, lane L's
-            // 16 B at slot 64 j + L = 4 m + (L & 3) for message m = 16 j + L / 4;
-            // that slot must hold quarter (L & 3) ^ ((m >> 2) & 3) (the XOR
-            // swizzle of lds_slot), and (m >> 2) & 3 = (L >> 4) & 3 for every j.
-            // Each message's 4 quarters are still fetched by 4 adjacent lanes
-            // (64 contiguous bytes).  A misaligned tile also DMAs the dword
-            // after each message's block window (the funnel's 17th dword) into
-            // my_extra[m], one dword per lane.
-            const uint32_t qd = (lane & 3u) ^ ((lane >> 4) & 3u);
-            uint32_t va[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                va[j] = ((uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) & ~3u) + 16u * qd;
-            const uint32_t ve = ((uint32_t)o & ~3u) + 64u;  // own message: dword after block 0's window
-            const uint32_t own_sel = be_sel((uint32_t)o & 3u);
-            typedef __attribute__((address_space(3))) void* lds_ptr_t;
-            auto dma = [&](uint32_t soff) {
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(my + 64 * j), 16, va[j], soff, 0, 0);
-                if (!aligned) __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)my_extra, 4, ve, soff, 0, 0);
-            };
-            MIRSHA_STAMP(t, 1);
-            dma(0u);
-            for (uint32_t blk = 0; blk < wave_nb; blk++) {
-                const uint32_t soff = 64u * blk;
-                // This wave's DMA of block blk has landed (LDS-DMA counts in vmcnt).
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (blk == 0u) MIRSHA_STAMP(t, 2);
-                uint32_t raw[17];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const uint4 x = my[lds_slot(lane, (uint32_t)k)];
-                    raw[4 * k + 0] = x.x; raw[4 * k + 1] = x.y; raw[4 * k + 2] = x.z; raw[4 * k + 3] = x.w;
-                }
-                raw[16] = aligned ? 0u : my_extra[lane];
-                // The reads completed before the next DMA overwrites the tile.
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#ifdef MIRSHA_AB_DMA_EARLY  // A/B build only: next block's DMA before this block's rounds
-                if (blk + 1u < wave_nb) dma(soff + 64u);
-#endif
-                uint32_t w[16];
-#pragma unroll
-                for (int k = 0; k < 16; k++) w[k] = be_word(raw[k + 1], raw[k], own_sel);
-                if (soff + 64u > min_l) {  // wave-uniform: a block past the wave's shortest message
-                    const bool last = blk + 1u == nb;
-#pragma unroll
-                    for (int k = 0; k < 4; k++) pad_words(soff + 16u * k, L, last, (uint32_t)k, &w[4 * k]);
-                }
-                if (blk == 0u) __builtin_amdgcn_s_setprio(0);
-                // Rounds on every lane (a lane past its message discards the
-                // result), so the DMA between the halves runs with all lanes:
-                // its lane roles are loader roles, not this lane's message.
-                // Issued half a compression ahead: enough to cover the load,
-                // and half the bytes in flight of a whole-block lead, which
-                // keeps the memory queues (and every other load) shorter.
-                uint32_t s8[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++) s8[i] = st[i];
-                rounds_asm_lo(s8, w);
-#ifndef MIRSHA_AB_DMA_EARLY
-                if (blk + 1u < wave_nb) dma(soff + 64u);
-#endif
-                rounds_asm_hi(s8, w);
-                if (blk < nb) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) st[i] += s8[i];
-                }
-            }
-            MIRSHA_STAMP(t, 3);
-#ifdef MIRSHA_AB_STAMPS
-            {
-                unsigned hw, xcc;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                if (lane == 0u && t < kStampTiles) {
-                    g_stamps[kStampWords * t + 4] = hw;
-                    g_stamps[kStampWords * t + 5] = xcc;
-                }
-            }
-#endif
-            if (valid) store_digest(out, msg, st);
-            return;
-        }
-#endif
         uint32_t vo[4], sel[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -372,6 +296,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             vo[j] = a & ~3u;
             sel[j] = be_sel(a & 3u);
         }
+        MIRSHA_STAMP(t, 1);
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
             const uint32_t soff = 64u * blk;
             RawChunk rc[4];
@@ -419,9 +344,13 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef MIRSHA_AB_PRIO
             if (blk == 0u) __builtin_amdgcn_s_setprio(0);
+#endif
+            if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm(st, w);
         }
+        MIRSHA_STAMP_END(t);
     } else if constexpr (kLds) {
         // Wide arenas: the same LDS staging with per-chunk 64-bit addresses
         // and activity tests (one launch over > 4 GiB, BASELINE config 5).
@@ -458,7 +387,9 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifdef MIRSHA_AB_PRIO
             if (blk == 0u) __builtin_amdgcn_s_setprio(0);
+#endif
             if (blk < nb) compress_asm(st, w);
         }
     } else {
@@ -471,7 +402,9 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
+#ifdef MIRSHA_AB_PRIO
             if (blk == 0u) __builtin_amdgcn_s_setprio(0);
+#endif
             if (active) compress_asm(st, w);
         }
     }
@@ -494,12 +427,11 @@ __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : 8) void sha256_msgs_ker
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
     uint8_t* __restrict__ out) {
     __shared__ uint4 tile[kMsgWaves][256];
-    __shared__ uint32_t extra[kMsgWaves][64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * kMsgWaves + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<kLds, kWide>(arena, arena_len, off, len, order, n, out, tile[wv], extra[wv], t, lane);
+    hash_tile<kLds, kWide>(arena, arena_len, off, len, order, n, out, tile[wv], t, lane);
 }
 
 // Low-occupancy form of the request kernel, for launches of at most one wave

@@ -4,7 +4,7 @@ Every rank hashes a contiguous, batch-aligned request range on its own GPU
 (no collective in the data path: requests are independent, actions.go:22-23);
 digests are gathered to every rank in rank order, which is origin order.
 The gather is control-plane traffic (32 B per digest) over torch.distributed —
-gloo on CPU, RCCL ("nccl") on GPUs.
+gloo with CPU tensors, or RCCL ("nccl") with tensors on the rank's current GPU.
 """
 from __future__ import annotations
 
@@ -23,16 +23,18 @@ def _all_gather_rows(rows: np.ndarray, group=None) -> list:
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    n = torch.tensor([rows.shape[0]], dtype=torch.int64)
-    sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    # RCCL ("nccl") only moves device tensors; gloo moves CPU tensors.
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     m = max(int(s.item()) for s in sizes)
-    buf = torch.zeros((m, 32), dtype=torch.uint8)
+    buf = torch.zeros((m, 32), dtype=torch.uint8, device=dev)
     if rows.shape[0]:
-        buf[: rows.shape[0]] = torch.from_numpy(np.ascontiguousarray(rows))
-    outs = [torch.zeros((m, 32), dtype=torch.uint8) for _ in range(world)]
+        buf[: rows.shape[0]] = torch.from_numpy(np.ascontiguousarray(rows)).to(dev)
+    outs = [torch.zeros((m, 32), dtype=torch.uint8, device=dev) for _ in range(world)]
     dist.all_gather(outs, buf, group=group)
-    return [o[: int(s.item())].numpy() for o, s in zip(outs, sizes)]
+    return [o[: int(s.item())].cpu().numpy() for o, s in zip(outs, sizes)]
 
 
 def hash_sharded(hash_fn: HashFn, n_req: int, batch_size: int, lengths: Optional[np.ndarray] = None,

@@ -20,6 +20,7 @@ KERNEL_LISTS = 1
 KERNEL_GEN = 2
 KERNEL_CHAIN = 3
 KERNEL_FUSED = 4
+ASYNC_SLOTS = 4  # submissions in flight per context (mirsha_submit_slices)
 
 # mirsha_pipeline modes (include/mirsha.h)
 PIPELINE_SEQUENTIAL = 0
@@ -134,12 +135,18 @@ class Engine:
         self.ctx = ctx
         self.device = device
         self.last_unique = 0
+        # Output arrays of submissions the library has not retired yet: it
+        # writes the digests there inside mirsha_wait / mirsha_poll, or when a
+        # later submit retires the oldest of its ASYNC_SLOTS ring slots, so
+        # they must outlive a dropped Ticket.
+        self._outstanding: dict[int, np.ndarray] = {}
 
     # ------------------------------------------------------------ lifecycle
     def close(self) -> None:
         if getattr(self, "ctx", None):
-            self._lib.mirsha_ctx_destroy(self.ctx)
+            self._lib.mirsha_ctx_destroy(self.ctx)  # no digest is written after this
             self.ctx = None
+            self._outstanding = {}
 
     def __enter__(self):
         return self
@@ -259,15 +266,26 @@ class Engine:
         t = ctypes.c_uint64(0)
         self._check(self._lib.mirsha_submit_slices(self.ctx, sl.ptr_p, sl.len_p, sl.first_p, sl.n, _ptr(out),
                                                    _lib.MIRSHA_SUBMIT_DEDUP if dedup else 0, ctypes.byref(t)))
+        self._outstanding[t.value] = out
+        # Submission t took the ring slot of t - ASYNC_SLOTS, which the library
+        # completed (in order) before reusing it.
+        self._retire(t.value - ASYNC_SLOTS)
         return Ticket(t.value, out)
+
+    def _retire(self, upto: int) -> None:
+        for k in [k for k in self._outstanding if k <= upto]:
+            del self._outstanding[k]
 
     def wait(self, ticket: "Ticket") -> np.ndarray:
         self._check(self._lib.mirsha_wait(self.ctx, ticket.value))
+        self._retire(ticket.value)
         return ticket.out
 
     def poll(self, ticket: "Ticket") -> bool:
         done = ctypes.c_int(0)
         self._check(self._lib.mirsha_poll(self.ctx, ticket.value, ctypes.byref(done)))
+        if done.value:
+            self._retire(ticket.value)
         return bool(done.value)
 
     def hash_requests_then_batches(self, arena, off, length, idx, batch_first, out=None, batch_out=None):
@@ -337,6 +355,16 @@ class Engine:
     def synth_mixed_device(self, seed: int, first: int, count: int, d_off: int, d_arena: int) -> None:
         """Config-5 message bytes of requests [first, first + count) at d_arena + d_off[r]."""
         self._check(self._lib.mirsha_synth_mixed_device(self.ctx, seed, first, count, d_off, d_arena))
+
+    HOST_PHASES = ("validate", "plan", "pack", "device", "scatter")
+
+    def host_profile(self) -> dict:
+        """Host-side phases (ms) of the last slice submission (mirsha_ctx_host_profile)."""
+        buf = (ctypes.c_double * len(self.HOST_PHASES))()
+        n = self._lib.mirsha_ctx_host_profile(self.ctx, buf, len(self.HOST_PHASES))
+        if n < 0:
+            self._check(n)
+        return {k: buf[i] for i, k in enumerate(self.HOST_PHASES)}
 
     def clock_probe(self, iters: int = 128) -> tuple[float, float]:
         """(clock GHz held under the compression load, SIMD cycles per 64-lane

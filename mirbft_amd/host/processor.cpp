@@ -121,6 +121,26 @@ PendingResults Processor::Submit(const Actions& actions) {
     return p;
 }
 
+PendingResults& PendingResults::operator=(PendingResults&& o) noexcept {
+    if (this != &o) {
+        if (ticket_) {  // overwriting an uncollected cycle: let it land first
+            try { engine_->Wait(ticket_); } catch (...) {}
+        }
+        engine_ = o.engine_;
+        ticket_ = o.ticket_;
+        reqs_ = std::move(o.reqs_);
+        digests_ = std::move(o.digests_);
+        o.ticket_ = 0;
+    }
+    return *this;
+}
+
+PendingResults::~PendingResults() {
+    if (ticket_) {
+        try { engine_->Wait(ticket_); } catch (...) {}  // the buffer must outlive the library's write
+    }
+}
+
 ActionResults PendingResults::Wait() {
     if (ticket_) {
         engine_->Wait(ticket_);
@@ -149,7 +169,14 @@ extern "C" int mirbft_host_process_ex(int device, const uint8_t* const* data, co
             a.Hash.push_back(&reqs[i]);
         }
         mirbft::ActionResults r;
-        if (flags & 2) {
+        if (flags & 4) {
+            // A cycle dropped without Wait, then 4 more: the ring retires the
+            // dropped one while later submissions are queued.
+            { mirbft::PendingResults dropped = p.Submit(a); }
+            std::vector<mirbft::PendingResults> more;
+            for (int k = 0; k < 4; k++) more.push_back(p.Submit(a));
+            for (auto& m : more) r = m.Wait();
+        } else if (flags & 2) {
             mirbft::PendingResults pending = p.Submit(a);
             r = pending.Wait();
         } else {

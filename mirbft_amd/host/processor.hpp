@@ -91,8 +91,17 @@ private:
 std::unique_ptr<Hash> NewGpuSha256(GpuEngine& engine);
 
 // One submitted cycle; Wait() returns its ActionResults (origin order).
+// Owns the buffer the library writes the digests into (inside mirsha_wait, or
+// when a later submission retires this one's ring slot), so it is move-only
+// and its destructor waits for a cycle that was never collected.
 class PendingResults {
 public:
+    PendingResults() = default;
+    PendingResults(PendingResults&& o) noexcept { *this = std::move(o); }
+    PendingResults& operator=(PendingResults&& o) noexcept;
+    PendingResults(const PendingResults&) = delete;
+    PendingResults& operator=(const PendingResults&) = delete;
+    ~PendingResults();
     ActionResults Wait();
 
 private:
@@ -123,7 +132,8 @@ extern "C" {
 // mirbft::Processor (exercises the C++ mirror end to end).
 int mirbft_host_process(int device, const uint8_t* const* data, const uint64_t* len, uint32_t n,
                         uint8_t* digests_out, char* err, uint32_t err_len);
-// flags: bit 0 = dedup, bit 1 = asynchronous (Submit, then Wait).
+// flags: bit 0 = dedup, bit 1 = asynchronous (Submit, then Wait), bit 2 =
+// asynchronous with a dropped (never waited) cycle before four more.
 int mirbft_host_process_ex(int device, const uint8_t* const* data, const uint64_t* len, uint32_t n,
                            uint8_t* digests_out, int flags, uint32_t* unique_out, char* err, uint32_t err_len);
 }

@@ -129,7 +129,7 @@ def test_work_pool_overlap(engine):
     assert [x.request for x in r.digests] == reqs
 
 
-@pytest.mark.parametrize("flags", [1, 2, 3])
+@pytest.mark.parametrize("flags", [1, 2, 3, 4, 5])
 def test_cpp_mirror_dedup_async(flags):
     host = ctypes.CDLL(_lib.HOST_LIB_PATH)
     msgs = [b"m" * (i % 7) * 50 for i in range(100)]
@@ -147,3 +147,53 @@ def test_cpp_mirror_dedup_async(flags):
     got = [bytes(out[32 * i: 32 * i + 32]) for i in range(len(msgs))]
     assert got == [hashlib.sha256(m).digest() for m in msgs]
     assert uniq.value == (7 if flags & 1 else len(msgs))
+
+
+def test_config4_full_scale_epoch_change_cycle(engine):
+    """BASELINE config 4 at its stated scale: a 64-node network's epoch change
+    (mirbft.go:125-154: CheckpointInterval 320), one node's Ready() cycle =
+    64 origins x 64 relaying sources of EpochChangeAck hash requests
+    (applyEpochChangeAckMsg, epoch_target.go:459-477), each the
+    epochChangeHashData slices of its origin's EpochChange
+    (stateless.go:311-340): C = 3 checkpoints, |P| = |Q| = 640 entries,
+    61,568-byte payloads of 3,847 slices, every ack its own copy (252 MB).
+    Every digest, in origin order, equals hashlib over that origin's payload,
+    through the dedup entry point, the plain one and the async submit."""
+    n_nodes, n_req, cps, np_, nq = 64, 4096, 3, 640, 640
+    buf, so, sl, first, origin = hashdata.epoch_change_cycle(n_nodes, n_req, cps, np_, nq)
+    plen = buf.size // n_req
+    assert plen == 8 + cps * 40 + (np_ + nq) * 48 == 61_568
+    assert int(first[1]) == 1 + 2 * cps + 3 * (np_ + nq) == 3_847
+    arrays = SliceArrays.from_buffer(buf, so, sl, first)
+    payload = [hashlib.sha256(hashdata.concat(hashdata.epoch_change_payload(2, o, cps, np_, nq))).digest()
+               for o in range(n_nodes)]
+    expect = [payload[o] for o in origin]
+    # the bytes of every ack are the origin's payload (not only equal digests)
+    for r in (0, 1, 63, 64, 4095):
+        assert hashlib.sha256(buf[r * plen:(r + 1) * plen].tobytes()).digest() == payload[origin[r]]
+    got = engine.hash_slice_arrays(arrays, dedup=True)
+    assert engine.last_unique == n_nodes
+    assert rows(got) == expect
+    prof = engine.host_profile()
+    assert prof["plan"] > 0 and prof["device"] > 0
+    plain = engine.hash_slice_arrays(arrays, dedup=False)
+    assert engine.last_unique == n_req
+    assert rows(plain) == expect
+    t = engine.submit_slices(arrays, dedup=True)
+    assert rows(engine.wait(t)) == expect
+
+
+def test_dropped_ticket_then_four_more(engine):
+    """a ticket dropped without wait() is retired by a later submit
+    writing its digests; the engine keeps that output alive until then."""
+    import gc
+
+    reqs = [random_requests(s, n=64) for s in range(6)]
+    t0 = engine.submit_slices(reqs[0])
+    del t0
+    gc.collect()
+    ts = [engine.submit_slices(r) for r in reqs[1:5]]  # the 5th submission overall retires the dropped one
+    assert len(engine._outstanding) <= 4
+    for t, r in zip(ts, reqs[1:5]):
+        assert rows(engine.wait(t)) == want(r)
+    assert not engine._outstanding
