@@ -220,18 +220,20 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
                                           uint4* my, uint32_t t, uint32_t lane) {
     MIRSHA_STAMP(t, 0);
-    // The prologue stays at the default issue priority: a fresh wave is the
-    // youngest on its SIMD and issues when older ones stall.  Raising it
-    // (s_setprio 3 until the first compression) got the new waves computing
-    // sooner but measured 1 % slower (profiles/r02g).
-#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 prologue (conditional loads)
+    // Prologue at the highest issue priority, back to 0 at the first
+    // compression: a fresh wave is the youngest on its SIMD and at the default
+    // priority gets the VALU only when every older wave stalls, so its
+    // metadata loads and first block took ~20 us of a ~60-90 us wave life
+    // (tools/stamp_run.py).  Same-box A/B (profiles/r02h): 196.4 us per
+    // config-2 launch vs 201.9 us without.
+#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 prologue (conditional loads, default priority)
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
     const uint32_t L = valid ? len[msg] : 0u;
     const uint64_t o = valid ? off[msg] : 0u;
 #else
-#ifdef MIRSHA_AB_PRIO  // A/B build only: high-priority prologue
+#ifndef MIRSHA_AB_NOPRIO  // A/B build only: default-priority prologue
     __builtin_amdgcn_s_setprio(3);
 #endif
     const uint32_t slot = t * 64u + lane;
@@ -344,7 +346,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef MIRSHA_AB_PRIO
+#ifndef MIRSHA_AB_NOPRIO
             if (blk == 0u) __builtin_amdgcn_s_setprio(0);
 #endif
             if (blk == 0u) MIRSHA_STAMP(t, 2);
@@ -387,7 +389,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef MIRSHA_AB_PRIO
+#ifndef MIRSHA_AB_NOPRIO
             if (blk == 0u) __builtin_amdgcn_s_setprio(0);
 #endif
             if (blk < nb) compress_asm(st, w);
@@ -402,7 +404,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
-#ifdef MIRSHA_AB_PRIO
+#ifndef MIRSHA_AB_NOPRIO
             if (blk == 0u) __builtin_amdgcn_s_setprio(0);
 #endif
             if (active) compress_asm(st, w);

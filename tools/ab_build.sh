@@ -5,7 +5,7 @@
 #   r1form:    -DMIRSHA_AB_KSGPR -DMIRSHA_AB_NOALIGNED -DMIRSHA_AB_OLDPROLOGUE
 #              (round constants in SGPRs, 5-dword chunks, round-1 prologue)
 #   oldpro:    -DMIRSHA_AB_OLDPROLOGUE  (shuffle reductions, conditional metadata loads)
-#   prio:      -DMIRSHA_AB_PRIO         (s_setprio 3 from wave start to the first compression)
+#   noprio:    -DMIRSHA_AB_NOPRIO       (request prologue at the default issue priority)
 #   wg4:       -DMIRSHA_AB_WG4          (4-wave request workgroups)
 #   stamps:    -DMIRSHA_AB_STAMPS       (per-tile timeline for tools/stamp_run.py)
 set -euo pipefail
@@ -19,7 +19,7 @@ build() {
 }
 build r1form -DMIRSHA_AB_KSGPR -DMIRSHA_AB_NOALIGNED -DMIRSHA_AB_OLDPROLOGUE &
 build oldpro -DMIRSHA_AB_OLDPROLOGUE &
-build prio -DMIRSHA_AB_PRIO &
+build noprio -DMIRSHA_AB_NOPRIO &
 build wg4 -DMIRSHA_AB_WG4 &
 build stamps -DMIRSHA_AB_STAMPS &
 wait
