@@ -71,7 +71,8 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=100,
                    help="untimed steps; MI355X needs ~20+ ms of sustained load to reach its working clock")
-    p.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    p.add_argument("--config", type=int, default=2, choices=[1] + sorted(CONFIGS),
+                   help="BASELINE config (1 = small-cycle latency of the host API)")
     p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
     p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6],
                    help="0 = LDS-staged loader (latency forms for small launches), 1 = direct per-lane loads, "
@@ -541,6 +542,82 @@ class EpochChangeWorkload:
         return {"pcie_inclusive_by_design": True}
 
 
+def small_cycle_bench(a, eng):
+    """Config 1 (testengine, 4 nodes x 4 clients x 200 requests, BatchSize 20):
+    a Ready() cycle's Actions.Hash is tens of request hashes -- LE64(client) ||
+    LE64(reqNo) || data, data = LE64(client) || "-" || LE64(reqNo), 3 slices,
+    33 bytes (state_machine.go:313-317, testengine/recorder.go:158-174) --
+    plus batch hashes over 20 RequestAck digests (sequence.go:154-157, 20
+    slices of 32 B), all independent HashRequests of one call.  Per-call
+    latency (median / p90 over `reps` calls) of the synchronous host API
+    (mirsha_hash_slices), the asynchronous one (submit + wait) and the one-core
+    CPU port of the loop on the same slices."""
+    from mirbft_amd import SliceArrays
+
+    o = _oracle()
+    reps, rows = 300, []
+    for n_req in (16, 80, 320):
+        n_bat = max(1, n_req // 20)
+        buf = np.zeros(33 * n_req + 32 * 20 * n_bat, dtype=np.uint8)
+        so, sl, first = [], [], [0]
+        for i in range(n_req):
+            c, r = i % 4, i // 4
+            b = 33 * i
+            buf[b:b + 8] = np.frombuffer(np.uint64(c).tobytes(), np.uint8)
+            buf[b + 8:b + 16] = np.frombuffer(np.uint64(r).tobytes(), np.uint8)
+            buf[b + 16:b + 24] = buf[b:b + 8]
+            buf[b + 24] = ord("-")
+            buf[b + 25:b + 33] = buf[b + 8:b + 16]
+            so += [b, b + 8, b + 16]
+            sl += [8, 8, 17]
+            first.append(len(so))
+        rng = np.random.default_rng(n_req)
+        base = 33 * n_req
+        buf[base:] = rng.integers(0, 256, buf.size - base, dtype=np.uint8)
+        for k in range(n_bat):
+            for j in range(20):
+                so.append(base + 32 * (20 * k + j))
+                sl.append(32)
+            first.append(len(so))
+        arrays = SliceArrays.from_buffer(buf, np.array(so, np.uint64), np.array(sl, np.uint64), np.array(first, np.uint32))
+        n = arrays.n
+        want = o.hash_slices(arrays.ptr, arrays.len, arrays.first)
+        got = eng.hash_slice_arrays(arrays)
+        assert np.array_equal(got, want), "small-cycle digests differ from the oracle"
+
+        def lat(fn):
+            for _ in range(20):
+                fn()
+            t = np.empty(reps)
+            for k in range(reps):
+                t0 = time.perf_counter()
+                fn()
+                t[k] = time.perf_counter() - t0
+            return float(np.median(t) * 1e6), float(np.percentile(t, 90) * 1e6)
+
+        out = np.empty((n, 32), np.uint8)
+        sync = lat(lambda: eng.hash_slice_arrays(arrays))
+        asyn = lat(lambda: eng.wait(eng.submit_slices(arrays)))
+        cpu = lat(lambda: o.hash_slices(arrays.ptr, arrays.len, arrays.first, out))
+        rows.append({"request_hashes": n_req, "batch_hashes": n_bat, "hash_requests": n,
+                     "hash_slices_us": sync[0], "hash_slices_p90_us": sync[1],
+                     "submit_wait_us": asyn[0], "submit_wait_p90_us": asyn[1],
+                     "cpu_1core_us": cpu[0], "cpu_1core_p90_us": cpu[1]})
+    last = rows[-1]
+    print(json.dumps({
+        "metric": "Ready()-cycle hash latency, small testengine cycles (BASELINE config 1 shape)",
+        "value": last["hash_requests"] / (last["hash_slices_us"] * 1e-6), "unit": "digests/s",
+        "n_gpus": 1, "steps": reps, "warmup": 20, "ms_per_step": last["hash_slices_us"] / 1e3,
+        "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic testengine requests (recorder.go:158-174) + random RequestAck digests",
+        "config": {"workload": "config1: tens of 33-B request hashes + BatchSize-20 batch hashes per Ready() cycle, "
+                               "host slices through the C-ABI, synchronous and asynchronous"},
+        "cycles": rows,
+        "note": "per-call wall time from host slices to host digests (PCIe both ways, kernel launch, one sync); "
+                "cpu_1core = oracle C port of processor.go:133-143 (SHA-NI) on the same slices",
+    }), flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -558,6 +635,9 @@ def main():
 
     eng = Engine(local)
     eng.set_variant(a.variant)
+    if a.config == 1:  # latency of small host-API cycles (own JSON line)
+        small_cycle_bench(a, eng)
+        return
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
 

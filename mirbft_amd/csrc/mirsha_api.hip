@@ -24,7 +24,10 @@
 
 namespace {
 
-constexpr uint64_t kPackWindow = 256ull << 20;  // bytes per packed H2D chunk
+constexpr uint64_t kStageChunk = 32ull << 20;  // pinned staging chunk for pageable request bytes
+constexpr int kStageSlots = 3;                  // chunks in flight (packed while earlier ones DMA)
+constexpr uint64_t kInlineArena = 1ull << 20;   // arenas up to this ride in the metadata copy
+constexpr uint64_t kPinnedOutMax = 8ull << 20;  // digest results up to this come back via pinned staging
 constexpr uint64_t kArenaSlack = 256;           // loader may touch up to 80 B past a message
 constexpr uint32_t kFusedMaxListWaves = 64;      // chain waves of a fused launch (16 CUs)
 constexpr uint32_t kFusedMinChainBlocks = 64;    // AUTO picks the fused launch from this chain length
@@ -109,7 +112,14 @@ struct mirsha_ctx {
     uint32_t time_mask = 0xFFFFFFFFu;  // kernels timed while timing is on
     std::string err;
     DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
-    PinnedBuf h_stage;
+    // Staged host calls (see "staged host calls" below): a ring of pinned
+    // chunks for pageable request bytes, one pinned metadata block (plus small
+    // arenas) -> one H2D, and pinned digest staging for small results.
+    PinnedBuf h_ring[kStageSlots];
+    hipEvent_t ring_ev[kStageSlots] = {};
+    bool ring_busy[kStageSlots] = {};
+    PinnedBuf h_meta, h_outs;
+    DevBuf d_meta;
     KernelTimer timers[6];         // msgs, lists, gen, chain, fused, (5: retired)
     AsyncSlot slots[kAsyncSlots];
     uint64_t next_ticket = 1;  // ticket of the next submission
@@ -234,87 +244,6 @@ bool bucket_order(const uint32_t* len, uint32_t n, uint32_t* order) {
     return false;
 }
 
-// Hash n messages whose bytes are in device memory at d_arena (offsets
-// relative to it), writing digests to d_out (device, origin order).
-int hash_resident(mirsha_ctx* c, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* h_off,
-                  const uint32_t* h_len, uint32_t n, uint8_t* d_out) {
-    HIP_TRY(c, c->d_off.ensure(sizeof(uint64_t) * n));
-    HIP_TRY(c, c->d_len.ensure(sizeof(uint32_t) * n));
-    std::vector<uint32_t> order(n);
-    const bool identity = bucket_order(h_len, n, order.data());
-    HIP_TRY(c, hipMemcpyAsync(c->d_off.p, h_off, sizeof(uint64_t) * n, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(c->d_len.p, h_len, sizeof(uint32_t) * n, hipMemcpyHostToDevice, c->stream));
-    const uint32_t* d_order = nullptr;
-    if (!identity) {
-        HIP_TRY(c, c->d_order.ensure(sizeof(uint32_t) * n));
-        HIP_TRY(c, hipMemcpyAsync(c->d_order.p, order.data(), sizeof(uint32_t) * n,
-                                  hipMemcpyHostToDevice, c->stream));
-        d_order = c->d_order.as<uint32_t>();
-    }
-    int rc = timed_launch(c, 0, [&] {
-        return mirsha::launch_msgs(d_arena, arena_len, c->d_off.as<uint64_t>(),
-                                   c->d_len.as<uint32_t>(), d_order, n, d_out, c->variant, c->stream);
-    });
-    if (rc) return rc;
-    // The host vectors above must outlive the async copies.
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return MIRSHA_OK;
-}
-
-// Digests of n host messages into device buffer d_out (n*32 bytes).
-// Copies the arena span directly when it is dense, otherwise packs messages
-// into pinned staging windows.
-int hash_host_messages(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
-                       const uint32_t* len, uint32_t n, uint8_t* d_out) {
-    if (n == 0) return MIRSHA_OK;
-    uint64_t lo = UINT64_MAX, hi = 0, total = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        if (len[i] > MIRSHA_MAX_MESSAGE_BYTES)
-            return fail(c, MIRSHA_ERANGE, "message %u is %u bytes (max %u)", i, len[i], MIRSHA_MAX_MESSAGE_BYTES);
-        if (off[i] > arena_len || len[i] > arena_len - off[i])
-            return fail(c, MIRSHA_EINVAL, "message %u [%llu,+%u) outside arena of %llu bytes", i,
-                        (unsigned long long)off[i], len[i], (unsigned long long)arena_len);
-        lo = std::min<uint64_t>(lo, off[i]);
-        hi = std::max<uint64_t>(hi, off[i] + len[i]);
-        total += len[i];
-    }
-    const uint64_t span = hi - lo;
-    if (span + kArenaSlack <= MIRSHA_MAX_DEVICE_ARENA_BYTES && span <= 2 * total + 4096) {
-        // Dense: one H2D copy of the span, offsets rebased.
-        HIP_TRY(c, c->d_arena.ensure(span + kArenaSlack));
-        if (span)
-            HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, arena + lo, span, hipMemcpyHostToDevice, c->stream));
-        std::vector<uint64_t> roff(off, off + n);
-        if (lo)
-            for (auto& x : roff) x -= lo;
-        return hash_resident(c, c->d_arena.as<uint8_t>(), span, roff.data(), len, n, d_out);
-    }
-    // Sparse or huge: pack consecutive messages into windows.
-    uint32_t i = 0;
-    while (i < n) {
-        uint64_t bytes = 0;
-        uint32_t j = i;
-        while (j < n && (j == i || bytes + len[j] <= kPackWindow)) bytes += len[j++];
-        HIP_TRY(c, c->h_stage.ensure(bytes + kArenaSlack));
-        HIP_TRY(c, c->d_arena.ensure(bytes + kArenaSlack));
-        std::vector<uint64_t> poff(j - i);
-        uint64_t p = 0;
-        uint8_t* st = c->h_stage.as<uint8_t>();
-        for (uint32_t k = i; k < j; k++) {
-            poff[k - i] = p;
-            if (len[k]) memcpy(st + p, arena + off[k], len[k]);
-            p += len[k];
-        }
-        if (bytes)
-            HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, st, bytes, hipMemcpyHostToDevice, c->stream));
-        int rc = hash_resident(c, c->d_arena.as<uint8_t>(), bytes, poff.data(), len + i, j - i,
-                               d_out + 32ull * i);
-        if (rc) return rc;
-        i = j;
-    }
-    return MIRSHA_OK;
-}
-
 int check_lists(mirsha_ctx* c, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
                 uint32_t n_digests) {
     if (!first) return fail(c, MIRSHA_EINVAL, "list_first is NULL");
@@ -335,20 +264,221 @@ int check_lists(mirsha_ctx* c, const uint32_t* idx, const uint32_t* first, uint3
     return MIRSHA_OK;
 }
 
-// Digest lists over device-resident digests d_digests; writes d_out (device).
-int lists_resident(mirsha_ctx* c, const uint8_t* d_digests, uint32_t n_digests, const uint32_t* idx,
-                   const uint32_t* first, uint32_t n_lists, uint8_t* d_out) {
-    const uint32_t entries = first[n_lists];
-    HIP_TRY(c, c->d_first.ensure(sizeof(uint32_t) * (n_lists + 1)));
-    HIP_TRY(c, c->d_idx.ensure(sizeof(uint32_t) * std::max<uint32_t>(entries, 1)));
-    HIP_TRY(c, hipMemcpyAsync(c->d_first.p, first, sizeof(uint32_t) * (n_lists + 1), hipMemcpyHostToDevice, c->stream));
-    if (entries)
-        HIP_TRY(c, hipMemcpyAsync(c->d_idx.p, idx, sizeof(uint32_t) * entries, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, c->d_scratch.ensure(sizeof(uint32_t) * std::max<uint32_t>(entries, 1)));
-    return timed_launch(c, 1, [&] {
-        return mirsha::launch_lists(d_digests, n_digests, c->d_idx.as<uint32_t>(), entries, c->d_first.as<uint32_t>(),
-                                    n_lists, c->d_scratch.as<uint32_t>(), d_out, c->stream);
-    });
+// ---- staged host calls --------------------------------------------------------
+//
+// The synchronous host API (the Go drop-in's path: one call per Ready()
+// cycle) moves the cycle's request bytes to HBM at PCIe rate and everything
+// else in ONE copy each way:
+//   - request bytes: DMA'd straight from a page-locked caller arena
+//     (mirsha_host_alloc), else packed by host threads into a ring of pinned
+//     chunks, each chunk's DMA overlapping the packing of the next; small
+//     arenas ride in the metadata copy;
+//   - metadata (offsets, lengths, bucket order, list indices): one pinned
+//     block, one H2D;
+//   - digests (requests, then lists, contiguous on the device): one D2H
+//     (through pinned staging when small);
+//   - one stream synchronisation per call.
+// Round 1 made 3-6 separate copies from pageable vectors plus two
+// synchronisations per call.
+
+// The bytes to hash, as the packed arena [0, total).
+struct ArenaSrc {
+    const uint8_t* base = nullptr;        // contiguous: arena byte x = base[x]; or
+    const uint8_t* const* ptr = nullptr;  // slice lists: request i = its slices, at poff[i]
+    const uint64_t* slen = nullptr;
+    const uint32_t* sfirst = nullptr;
+    const uint64_t* poff = nullptr;
+    uint32_t n = 0;
+    uint64_t total = 0;
+};
+
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+void fill(const ArenaSrc& src, uint64_t a, uint64_t b, uint8_t* dst) {
+    mirsha::host::pack_range(src.base, src.ptr, src.slen, src.sfirst, src.n, src.poff, a, b, dst,
+                             mirsha::host::threads_for(b - a, 1u << 20));
+}
+
+// Queues src's bytes into d_arena on c->stream (large arenas; small ones are
+// inlined by the caller).  Returns after the last chunk's DMA is queued.
+int h2d_arena(mirsha_ctx* c, const ArenaSrc& src, uint8_t* d_arena) {
+    if (src.total == 0) return MIRSHA_OK;
+    if (src.base && host_pinned(src.base)) {  // page-locked caller arena: one DMA from it
+        HIP_TRY(c, hipMemcpyAsync(d_arena, src.base, src.total, hipMemcpyHostToDevice, c->stream));
+        return MIRSHA_OK;
+    }
+    for (uint64_t a = 0, k = 0; a < src.total; a += kStageChunk, k++) {
+        const int slot = (int)(k % kStageSlots);
+        const uint64_t b = std::min(src.total, a + kStageChunk);
+        if (!c->ring_ev[slot]) HIP_TRY(c, hipEventCreateWithFlags(&c->ring_ev[slot], hipEventDisableTiming));
+        if (c->ring_busy[slot]) HIP_TRY(c, hipEventSynchronize(c->ring_ev[slot]));  // its previous DMA is done
+        HIP_TRY(c, c->h_ring[slot].ensure(kStageChunk));
+        fill(src, a, b, c->h_ring[slot].as<uint8_t>());
+        HIP_TRY(c, hipMemcpyAsync(d_arena + a, c->h_ring[slot].p, b - a, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ring_ev[slot], c->stream));
+        c->ring_busy[slot] = true;
+    }
+    return MIRSHA_OK;
+}
+
+// Layout of the per-call metadata block (pinned and on device).
+struct MetaLayout {
+    uint64_t off, len, order, idx, first, arena, end;
+    MetaLayout(uint32_t n, bool ordered, uint32_t entries, uint32_t n_lists, uint64_t inline_arena) {
+        auto al = [](uint64_t x) { return (x + 15u) & ~15ull; };
+        off = 0;
+        len = al(off + 8ull * n);
+        order = al(len + 4ull * n);
+        idx = al(order + (ordered ? 4ull * n : 0));
+        first = al(idx + 4ull * entries);
+        arena = al(first + (n_lists ? 4ull * (n_lists + 1) : 0));
+        end = al(arena + inline_arena + (inline_arena ? kArenaSlack : 0));
+    }
+};
+
+// One synchronous call: n messages (offsets relative to the packed arena) and
+// optionally n_lists digest lists over their digests.  req_out / list_out are
+// the caller's host buffers (n x 32, n_lists x 32).
+int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const uint32_t* len, uint32_t n,
+               const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint8_t* req_out, uint8_t* list_out) {
+    const uint32_t entries = n_lists ? first[n_lists] : 0u;
+    const bool inl = src.total <= kInlineArena;
+    // Large arenas first: their chunks DMA while the metadata is built.
+    HIP_TRY(c, c->d_arena.ensure(inl ? 1 : src.total + kArenaSlack));
+    if (!inl)
+        if (int rc = h2d_arena(c, src, c->d_arena.as<uint8_t>())) return rc;
+    std::vector<uint32_t> order_tmp;
+    uint32_t lo_b = UINT32_MAX, hi_b = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t b = host_blocks(len[i]);
+        lo_b = std::min(lo_b, b);
+        hi_b = std::max(hi_b, b);
+    }
+    const bool ordered = n && lo_b != hi_b;
+    const MetaLayout L(n, ordered, entries, n_lists, inl ? src.total : 0);
+    HIP_TRY(c, c->h_meta.ensure(L.end));
+    HIP_TRY(c, c->d_meta.ensure(L.end));
+    uint8_t* h = c->h_meta.as<uint8_t>();
+    if (n) {
+        memcpy(h + L.off, off, 8ull * n);
+        memcpy(h + L.len, len, 4ull * n);
+        if (ordered) bucket_order(len, n, reinterpret_cast<uint32_t*>(h + L.order));
+    }
+    if (entries) memcpy(h + L.idx, idx, 4ull * entries);
+    if (n_lists) memcpy(h + L.first, first, 4ull * (n_lists + 1));
+    if (inl && src.total) fill(src, 0, src.total, h + L.arena);
+    HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.end, hipMemcpyHostToDevice, c->stream));
+    uint8_t* dm = c->d_meta.as<uint8_t>();
+    const uint8_t* d_arena = inl ? dm + L.arena : c->d_arena.as<uint8_t>();
+    // Digests: requests then lists, contiguous (one D2H).
+    const uint64_t out_bytes = 32ull * ((uint64_t)n + n_lists);
+    HIP_TRY(c, c->d_out.ensure(std::max<uint64_t>(out_bytes, 32)));
+    uint8_t* d_req = c->d_out.as<uint8_t>();
+    uint8_t* d_lst = d_req + 32ull * n;
+    if (n) {
+        if (int rc = timed_launch(c, 0, [&] {
+                return mirsha::launch_msgs(d_arena, src.total, reinterpret_cast<const uint64_t*>(dm + L.off),
+                                           reinterpret_cast<const uint32_t*>(dm + L.len),
+                                           ordered ? reinterpret_cast<const uint32_t*>(dm + L.order) : nullptr, n,
+                                           d_req, c->variant, c->stream);
+            }))
+            return rc;
+    }
+    if (n_lists) {
+        // Lists index the request digests just computed, or with no requests
+        // the arena itself as 32-byte digests (mirsha_digest_lists).
+        const uint8_t* d_dig = n ? d_req : d_arena;
+        const uint32_t n_dig = n ? n : (uint32_t)(src.total / 32u);
+        HIP_TRY(c, c->d_scratch.ensure(sizeof(uint32_t) * std::max<uint32_t>(entries, 1)));
+        if (int rc = timed_launch(c, 1, [&] {
+                return mirsha::launch_lists(d_dig, n_dig, reinterpret_cast<const uint32_t*>(dm + L.idx), entries,
+                                            reinterpret_cast<const uint32_t*>(dm + L.first), n_lists,
+                                            c->d_scratch.as<uint32_t>(), d_lst, c->stream);
+            }))
+            return rc;
+    }
+    if (out_bytes <= kPinnedOutMax) {
+        HIP_TRY(c, c->h_outs.ensure(std::max<uint64_t>(out_bytes, 32)));
+        HIP_TRY(c, hipMemcpyAsync(c->h_outs.p, d_req, out_bytes, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (n) memcpy(req_out, c->h_outs.p, 32ull * n);
+        if (n_lists) memcpy(list_out, c->h_outs.as<uint8_t>() + 32ull * n, 32ull * n_lists);
+    } else {
+        if (n) HIP_TRY(c, hipMemcpyAsync(req_out, d_req, 32ull * n, hipMemcpyDeviceToHost, c->stream));
+        if (n_lists) HIP_TRY(c, hipMemcpyAsync(list_out, d_lst, 32ull * n_lists, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    for (bool& b : c->ring_busy) b = false;  // every queued chunk DMA has completed
+    return MIRSHA_OK;
+}
+
+// Validates messages of a caller arena; rebases them on the smallest offset.
+// Returns the dense span [lo, hi) or fails.
+int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uint32_t* len, uint32_t n,
+               uint64_t* lo_out, uint64_t* hi_out) {
+    uint64_t lo = n ? UINT64_MAX : 0, hi = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (len[i] > MIRSHA_MAX_MESSAGE_BYTES)
+            return fail(c, MIRSHA_ERANGE, "message %u is %u bytes (max %u)", i, len[i], MIRSHA_MAX_MESSAGE_BYTES);
+        if (off[i] > arena_len || len[i] > arena_len - off[i])
+            return fail(c, MIRSHA_EINVAL, "message %u [%llu,+%u) outside arena of %llu bytes", i,
+                        (unsigned long long)off[i], len[i], (unsigned long long)arena_len);
+        lo = std::min<uint64_t>(lo, off[i]);
+        hi = std::max<uint64_t>(hi, off[i] + len[i]);
+    }
+    *lo_out = lo;
+    *hi_out = hi;
+    return MIRSHA_OK;
+}
+
+// A caller arena + offsets: the span itself when dense, else the messages
+// packed back to back (sparse arenas do not ship their gaps).
+int run_arena_call(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off, const uint32_t* len,
+                   uint32_t n, const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint8_t* req_out,
+                   uint8_t* list_out) {
+    uint64_t lo = 0, hi = 0, total = 0;
+    if (int rc = arena_span(c, arena_len, off, len, n, &lo, &hi)) return rc;
+    for (uint32_t i = 0; i < n; i++) total += len[i];
+    std::vector<uint64_t> roff;
+    ArenaSrc src;
+    std::vector<const uint8_t*> sp;
+    std::vector<uint64_t> sl;
+    std::vector<uint32_t> sf;
+    if (hi - lo <= 2 * total + 4096) {  // dense: ship the span, offsets rebased
+        src.base = arena + lo;
+        src.total = hi - lo;
+        if (lo == 0) return run_staged(c, src, off, len, n, idx, first, n_lists, req_out, list_out);
+        roff.resize(n);
+        for (uint32_t i = 0; i < n; i++) roff[i] = off[i] - lo;
+    } else {  // sparse: one slice per message, packed
+        roff.resize(n);
+        sp.resize(n);
+        sl.resize(n);
+        sf.resize(n + 1);
+        uint64_t p = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            sp[i] = arena + off[i];
+            sl[i] = len[i];
+            sf[i] = i;
+            roff[i] = p;
+            p += len[i];
+        }
+        sf[n] = n;
+        src.ptr = sp.data();
+        src.slen = sl.data();
+        src.sfirst = sf.data();
+        src.poff = roff.data();
+        src.n = n;
+        src.total = total;
+    }
+    return run_staged(c, src, roff.data(), len, n, idx, first, n_lists, req_out, list_out);
 }
 
 // ---- request -> batch-digest plan (sequential form) ------------------------
@@ -843,7 +973,13 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     }
     c->d_arena.release(); c->d_off.release(); c->d_len.release(); c->d_order.release();
     c->d_out.release(); c->d_idx.release(); c->d_first.release(); c->d_out2.release(); c->d_scratch.release();
-    c->h_stage.release();
+    for (int k = 0; k < kStageSlots; k++) {
+        c->h_ring[k].release();
+        if (c->ring_ev[k]) (void)hipEventDestroy(c->ring_ev[k]);
+    }
+    c->h_meta.release();
+    c->h_outs.release();
+    c->d_meta.release();
     for (auto& sl : c->slots) {
         sl.stage.release(); sl.dig.release(); sl.dev.release();
         if (sl.done) (void)hipEventDestroy(sl.done);
@@ -923,11 +1059,7 @@ int mirsha_hash_batch(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, c
     if (n == 0) return MIRSHA_OK;
     if (!off || !len || !out || (!arena && arena_len)) return fail(c, MIRSHA_EINVAL, "NULL argument");
     if (int rc = use_device(c)) return rc;
-    HIP_TRY(c, c->d_out.ensure(32ull * n));
-    if (int rc = hash_host_messages(c, arena, arena_len, off, len, n, c->d_out.as<uint8_t>())) return rc;
-    HIP_TRY(c, hipMemcpyAsync(out, c->d_out.p, 32ull * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return MIRSHA_OK;
+    return run_arena_call(c, arena, arena_len, off, len, n, nullptr, nullptr, 0, out, nullptr);
 }
 
 
@@ -938,36 +1070,22 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
     std::vector<uint32_t> len;
     if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     if (int rc = use_device(c)) return rc;
-    // One packing pass into pinned memory (the Go side's single copy, in
-    // parallel for large cycles), then the common path; windows bound the
-    // staging footprint.
-    HIP_TRY(c, c->d_out.ensure(32ull * n));
-    uint32_t i = 0;
-    while (i < n) {
-        uint64_t bytes = 0;
-        uint32_t j = i;
-        while (j < n && (j == i || bytes + len[j] <= kPackWindow)) bytes += len[j++];
-        HIP_TRY(c, c->h_stage.ensure(bytes + kArenaSlack));
-        HIP_TRY(c, c->d_arena.ensure(bytes + kArenaSlack));
-        uint8_t* st = c->h_stage.as<uint8_t>();
-        std::vector<uint64_t> poff(j - i);
-        uint64_t p = 0;
-        for (uint32_t k = i; k < j; k++) {
-            poff[k - i] = p;
-            p += len[k];
-        }
-        mirsha::host::pack(slice_ptr, slice_len, slice_first + i, nullptr, j - i, poff.data(), st,
-                           mirsha::host::threads_for(bytes, j - i));
-        if (bytes)
-            HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, st, bytes, hipMemcpyHostToDevice, c->stream));
-        if (int rc = hash_resident(c, c->d_arena.as<uint8_t>(), bytes, poff.data(), len.data() + i, j - i,
-                                   c->d_out.as<uint8_t>() + 32ull * i))
-            return rc;
-        i = j;
+    // One packing pass, by threads, straight into pinned staging (the Go
+    // side's single copy), chunk by chunk behind the DMA of the previous one.
+    std::vector<uint64_t> poff(n);
+    uint64_t p = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        poff[i] = p;
+        p += len[i];
     }
-    HIP_TRY(c, hipMemcpyAsync(out, c->d_out.p, 32ull * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return MIRSHA_OK;
+    ArenaSrc src;
+    src.ptr = slice_ptr;
+    src.slen = slice_len;
+    src.sfirst = slice_first;
+    src.poff = poff.data();
+    src.n = n;
+    src.total = p;
+    return run_staged(c, src, poff.data(), len.data(), n, nullptr, nullptr, 0, out, nullptr);
 }
 
 int mirsha_host_alloc(mirsha_ctx* c, uint64_t bytes, void** out) {
@@ -1083,17 +1201,14 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
         pipeline_free(&p);
         return rc;
     }
-    // General path (sparse or windowed arena): all requests, then all lists.
-    if (int rc = hash_host_messages(c, arena, arena_len, off, len, n_req, c->d_out.as<uint8_t>())) return rc;
-    if (n_batches) {
-        HIP_TRY(c, c->d_out2.ensure(32ull * n_batches));
-        if (int rc = lists_resident(c, c->d_out.as<uint8_t>(), n_req, idx, first, n_batches, c->d_out2.as<uint8_t>()))
-            return rc;
-        HIP_TRY(c, hipMemcpyAsync(batch_out, c->d_out2.p, 32ull * n_batches, hipMemcpyDeviceToHost, c->stream));
+    // Staged path: request bytes at PCIe rate, metadata and digests in one
+    // copy each way, request kernel then list kernel.
+    if (n_req == 0 && n_batches == 0) return MIRSHA_OK;
+    if (n_req == 0) {  // lists of null requests only (every entry is MIRSHA_NULL_INDEX)
+        ArenaSrc none;
+        return run_staged(c, none, nullptr, nullptr, 0, idx, first, n_batches, nullptr, batch_out);
     }
-    if (n_req) HIP_TRY(c, hipMemcpyAsync(req_out, c->d_out.p, 32ull * n_req, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return MIRSHA_OK;
+    return run_arena_call(c, arena, arena_len, off, len, n_req, idx, first, n_batches, req_out, batch_out);
 }
 
 int mirsha_pipeline_create(mirsha_ctx* c, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
@@ -1179,15 +1294,10 @@ int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digest
     if (!out || (n_digests && !digests)) return fail(c, MIRSHA_EINVAL, "NULL argument");
     if (int rc = check_lists(c, idx, first, n_lists, n_digests)) return rc;
     if (int rc = use_device(c)) return rc;
-    HIP_TRY(c, c->d_arena.ensure(32ull * std::max<uint32_t>(n_digests, 1)));
-    if (n_digests)
-        HIP_TRY(c, hipMemcpyAsync(c->d_arena.p, digests, 32ull * n_digests, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, c->d_out2.ensure(32ull * n_lists));
-    if (int rc = lists_resident(c, c->d_arena.as<uint8_t>(), n_digests, idx, first, n_lists, c->d_out2.as<uint8_t>()))
-        return rc;
-    HIP_TRY(c, hipMemcpyAsync(out, c->d_out2.p, 32ull * n_lists, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    return MIRSHA_OK;
+    ArenaSrc src;  // the digests themselves are the arena the lists index
+    src.base = digests;
+    src.total = 32ull * n_digests;
+    return run_staged(c, src, nullptr, nullptr, 0, idx, first, n_lists, nullptr, out);
 }
 
 int mirsha_hash_batch_device(mirsha_ctx* c, const uint8_t* d_arena, uint64_t arena_len,

@@ -232,6 +232,44 @@ void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first,
     });
 }
 
+namespace {
+// Sequential body of pack_range over [a, b).
+void pack_range_seq(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                    const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst) {
+    if (a >= b) return;
+    // last request starting at or before a (poff nondecreasing)
+    uint32_t i = (uint32_t)(std::upper_bound(poff, poff + n, a) - poff);
+    i = i ? i - 1 : 0;
+    for (; i < n && poff[i] < b; i++) {
+        uint64_t p = poff[i];
+        for (uint32_t sl = first[i]; sl < first[i + 1] && p < b; sl++) {
+            const uint64_t L = len[sl];
+            const uint64_t lo = std::max(p, a), hi = std::min(p + L, b);
+            if (lo < hi) memcpy(dst + (lo - a), ptr[sl] + (lo - p), hi - lo);
+            p += L;
+        }
+    }
+}
+}  // namespace
+
+void pack_range(const uint8_t* base, const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first,
+                uint32_t n, const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst, int threads) {
+    if (a >= b) return;
+    const uint64_t total = b - a;
+    if (threads < 1) threads = 1;
+    const uint64_t piece = (total + threads - 1) / threads;
+    parallel_for((uint32_t)threads, threads, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t t = lo; t < hi; t++) {
+            const uint64_t x = a + std::min<uint64_t>(total, piece * t), y = a + std::min<uint64_t>(total, piece * (t + 1));
+            if (x >= y) continue;
+            if (!ptr)
+                memcpy(dst + (x - a), base + x, y - x);
+            else
+                pack_range_seq(ptr, len, first, n, poff, x, y, dst + (x - a));
+        }
+    });
+}
+
 }  // namespace host
 }  // namespace mirsha
 

@@ -44,5 +44,14 @@ uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32
 void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,
           uint32_t m, const uint64_t* dst_off, uint8_t* dst, int threads);
 
+// Bytes [a, b) of the packed arena of n requests -- request i = concat of its
+// slices [first[i], first[i+1]), placed at poff[i] (nondecreasing) -- into
+// dst (dst[0] = byte a), split over `threads` threads by byte range.  With
+// ptr == nullptr the source is the contiguous `base` instead (a parallel
+// memcpy of base[a, b)).  Used to fill one pinned staging chunk while the
+// previous chunk's DMA is in flight.
+void pack_range(const uint8_t* base, const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first,
+                uint32_t n, const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst, int threads);
+
 }  // namespace host
 }  // namespace mirsha

@@ -33,6 +33,7 @@ def load() -> ctypes.CDLL:
     vp = ctypes.c_void_p
     lib.oracle_hash_requests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
     lib.oracle_hash_requests_mt.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int]
+    lib.oracle_hash_slices.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
     lib.oracle_batch_digests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
     lib.oracle_gen_requests.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, vp]
     lib.oracle_sha256_force_impl.argtypes = [ctypes.c_int]
@@ -62,6 +63,16 @@ def hash_requests(arena, off, length, threads: int = 1) -> np.ndarray:
             lib.oracle_hash_requests_mt(_p(a), _p(o), _p(ln), o.size, _p(out), threads)
         else:
             lib.oracle_hash_requests(_p(a), _p(o), _p(ln), o.size, _p(out))
+    return out
+
+
+def hash_slices(slice_ptr: np.ndarray, slice_len: np.ndarray, first: np.ndarray, out: np.ndarray = None) -> np.ndarray:
+    """processor.go:133-143 over HashRequest.Data slice lists (addresses as uint64)."""
+    n = int(first.size) - 1
+    if out is None:
+        out = np.empty((n, 32), dtype=np.uint8)
+    if n:
+        load().oracle_hash_slices(_p(slice_ptr), _p(slice_len), _p(first), n, _p(out))
     return out
 
 

@@ -1,0 +1,43 @@
+"""The cgo call sequence of INTEGRATION.md's Go binding, made from C: gcc
+compiles tests/c/cgo_sequence.c against include/mirsha.h and links
+libmirsha.so (CPU test); on the GPU the program runs with no Python in the
+process and its digests are compared with the golden testengine request
+digests (tests/golden/layouts.json, hashlib-made from the reference's layouts,
+testengine/recorder.go:158-174 and state_machine.go:313-317)."""
+import os
+import subprocess
+
+import pytest
+
+from mirbft_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "c", "cgo_sequence.c")
+
+
+def build(out_dir) -> str:
+    exe = os.path.join(str(out_dir), "cgo_sequence")
+    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    SRC, "-L", _lib.LIB_DIR, "-lmirsha", "-Wl,-rpath," + _lib.LIB_DIR, "-o", exe], check=True)
+    return exe
+
+
+def test_cgo_sequence_compiles_and_links(tmp_path):
+    exe = build(tmp_path)
+    # every mirsha_* symbol the program calls resolves in libmirsha.so
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
+    assert "libmirsha.so" in ldd and "not found" not in ldd
+
+
+@pytest.mark.gpu
+def test_cgo_sequence_on_gpu(tmp_path, layouts):
+    exe = build(tmp_path)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert "fips ok" in lines and lines[-1] == "sequence ok"
+    want = {200 * e["client"] + e["req_no"]: e["sha256"] for e in layouts["testengine_requests"]}
+    assert len(want) == 800
+    for tag in ("req", "async"):
+        got = {int(i): h for t, i, h in (ln.split() for ln in lines if ln.startswith(tag + " "))}
+        assert got == want, tag
