@@ -276,15 +276,17 @@ class BatchWorkload:
             return (time.perf_counter() - t1) / reps
 
         pdt = rate(arena_h)
+        pprof = self.eng.host_profile()
         pinned = self.eng.host_empty(arena_h.size)
         pinned[:] = arena_h
         qdt = rate(pinned)
+        qprof = self.eng.host_profile()
         self.eng.set_stream(torch.cuda.current_stream(self.d_arena.device).cuda_stream)  # back to the steps' stream
         return {"digests_per_s": self.digests / pdt, "gb_per_s": self.bytes_hashed / pdt / 1e9,
-                "ms_per_call": pdt * 1e3,
+                "ms_per_call": pdt * 1e3, "host_phases_ms": pprof,
                 "note": "host API (pageable arena -> HBM -> digests -> reused host buffers), synchronous",
                 "pinned_arena": {"digests_per_s": self.digests / qdt, "gb_per_s": self.bytes_hashed / qdt / 1e9,
-                                 "ms_per_call": qdt * 1e3,
+                                 "ms_per_call": qdt * 1e3, "host_phases_ms": qprof,
                                  "note": "the same call on an arena from mirsha_host_alloc (page-locked)"}}
 
     def cpu_baseline(self, seconds):
@@ -506,6 +508,8 @@ class EpochChangeWorkload:
         return bool(ok)
 
     def pcie(self):
+        self.eng.hash_slice_arrays(self.sl, dedup=self.dedup)
+        self.host_phases = self.eng.host_profile()  # one cycle of the benched form
         other = not self.dedup
         reps, t0 = 5, time.perf_counter()
         for _ in range(reps):
@@ -539,7 +543,7 @@ class EpochChangeWorkload:
                 "compressions_per_step_per_gpu": self.req_blocks}
 
     def extra(self):
-        return {"pcie_inclusive_by_design": True}
+        return {"pcie_inclusive_by_design": True, "host_phases_ms": getattr(self, "host_phases", None)}
 
 
 def small_cycle_bench(a, eng):

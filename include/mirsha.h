@@ -167,13 +167,18 @@ int mirsha_submit_slices(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
 int mirsha_wait(mirsha_ctx* ctx, uint64_t ticket);
 int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
 
-/* Host-side phases (milliseconds) of the context's last slice submission
- * (mirsha_submit_slices / mirsha_hash_slices_dedup): validate = slice
- * lengths; plan = dedup plan (fingerprint + byte-for-byte confirm); pack =
- * gather into pinned staging + bucket order; device = queued -> complete (H2D,
- * kernel, D2H, plus any time the caller spent before waiting); scatter =
- * digests copied to the caller in origin order.  Writes min(n, phases)
- * entries; returns the number of phases. */
+/* Host-side phases (milliseconds) of the context's last host-API call.
+ * Slice submissions (mirsha_submit_slices / mirsha_hash_slices_dedup):
+ * validate = slice lengths; plan = dedup plan (fingerprint + byte-for-byte
+ * confirm); pack = gather into pinned staging + bucket order; device = queued
+ * -> complete (H2D, kernel, D2H, plus any time the caller spent before
+ * waiting); scatter = digests copied to the caller in origin order.
+ * Synchronous calls (mirsha_hash_batch / _slices / _requests_then_batches /
+ * mirsha_digest_lists): validate = arguments; pack = queueing the request
+ * bytes (pinned arena: one DMA; else packing into pinned chunks behind their
+ * DMA); plan = the metadata block; device = queue -> synchronised; scatter =
+ * digests to the caller.  Writes min(n, phases) entries; returns the number
+ * of phases. */
 #define MIRSHA_PROF_VALIDATE 0
 #define MIRSHA_PROF_PLAN 1
 #define MIRSHA_PROF_PACK 2

@@ -28,6 +28,11 @@ constexpr uint64_t kStageChunk = 32ull << 20;  // pinned staging chunk for pagea
 constexpr int kStageSlots = 3;                  // chunks in flight (packed while earlier ones DMA)
 constexpr uint64_t kInlineArena = 1ull << 20;   // arenas up to this ride in the metadata copy
 constexpr uint64_t kPinnedOutMax = 8ull << 20;  // digest results up to this come back via pinned staging
+// Small calls (a testengine-sized Ready() cycle) skip both copies: the kernels
+// read the pinned metadata block and write the digests to pinned memory over
+// PCIe (page-locked host memory is mapped into the GPU's address space), so
+// a call is one launch and one synchronisation.
+constexpr uint64_t kDirectMax = 256ull << 10;
 constexpr uint64_t kArenaSlack = 256;           // loader may touch up to 80 B past a message
 constexpr uint32_t kFusedMaxListWaves = 64;      // chain waves of a fused launch (16 CUs)
 constexpr uint32_t kFusedMinChainBlocks = 64;    // AUTO picks the fused launch from this chain length
@@ -292,6 +297,14 @@ struct ArenaSrc {
     uint64_t total = 0;
 };
 
+bool direct_small_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("MIRSHA_DIRECT_SMALL");  // 0: small calls copy both ways too (A/B)
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 bool host_pinned(const void* p) {
     hipPointerAttribute_t a;
     if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -299,6 +312,12 @@ bool host_pinned(const void* p) {
         return false;
     }
     return a.type == hipMemoryTypeHost;
+}
+
+// memcpy by host threads (multi-MB metadata and result copies).
+void pmemcpy(void* dst, const void* src, uint64_t n) {
+    mirsha::host::pack_range(static_cast<const uint8_t*>(src), nullptr, nullptr, nullptr, 0, nullptr, 0, n,
+                             static_cast<uint8_t*>(dst), mirsha::host::threads_for(n, 1u << 20));
 }
 
 void fill(const ArenaSrc& src, uint64_t a, uint64_t b, uint8_t* dst) {
@@ -328,6 +347,40 @@ int h2d_arena(mirsha_ctx* c, const ArenaSrc& src, uint8_t* d_arena) {
     return MIRSHA_OK;
 }
 
+// Device bytes [0, total) -> host: [0, split) to dst_a, [split, total) to
+// dst_b, through the pinned ring: chunk k+1's DMA runs while chunk k is
+// copied out by host threads (the caller's buffers are usually pageable).
+int d2h_split(mirsha_ctx* c, const uint8_t* d_src, uint64_t total, uint64_t split, uint8_t* dst_a, uint8_t* dst_b) {
+    const uint64_t nch = (total + kStageChunk - 1) / kStageChunk;
+    auto dst_at = [&](uint64_t x) { return x < split ? dst_a + x : dst_b + (x - split); };
+    auto queue = [&](uint64_t k) -> int {
+        const int slot = (int)(k % kStageSlots);
+        const uint64_t a = k * kStageChunk, b = std::min(total, a + kStageChunk);
+        if (!c->ring_ev[slot]) HIP_TRY(c, hipEventCreateWithFlags(&c->ring_ev[slot], hipEventDisableTiming));
+        HIP_TRY(c, c->h_ring[slot].ensure(kStageChunk));
+        HIP_TRY(c, hipMemcpyAsync(c->h_ring[slot].p, d_src + a, b - a, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipEventRecord(c->ring_ev[slot], c->stream));
+        return MIRSHA_OK;
+    };
+    for (uint64_t k = 0; k < std::min<uint64_t>(nch, kStageSlots - 1); k++)
+        if (int rc = queue(k)) return rc;
+    for (uint64_t k = 0; k < nch; k++) {
+        if (k + kStageSlots - 1 < nch)
+            if (int rc = queue(k + kStageSlots - 1)) return rc;
+        const int slot = (int)(k % kStageSlots);
+        HIP_TRY(c, hipEventSynchronize(c->ring_ev[slot]));
+        const uint64_t a = k * kStageChunk, b = std::min(total, a + kStageChunk);
+        const uint8_t* src = c->h_ring[slot].as<uint8_t>();
+        // split the chunk at the a/b boundary, copy each part with threads
+        const uint64_t m = std::min(std::max(split, a), b);
+        if (m > a) mirsha::host::pack_range(src - a, nullptr, nullptr, nullptr, 0, nullptr, a, m, dst_at(a),
+                                            mirsha::host::threads_for(m - a, 1u << 20));
+        if (b > m) mirsha::host::pack_range(src - a, nullptr, nullptr, nullptr, 0, nullptr, m, b, dst_at(m),
+                                            mirsha::host::threads_for(b - m, 1u << 20));
+    }
+    return MIRSHA_OK;
+}
+
 // Layout of the per-call metadata block (pinned and on device).
 struct MetaLayout {
     uint64_t off, len, order, idx, first, arena, end;
@@ -348,12 +401,18 @@ struct MetaLayout {
 // the caller's host buffers (n x 32, n_lists x 32).
 int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const uint32_t* len, uint32_t n,
                const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint8_t* req_out, uint8_t* list_out) {
+    // Host phases into c->prof (mirsha_ctx_host_profile): pack = queueing the
+    // request bytes, plan = metadata block, device = queue -> sync, scatter =
+    // digests to the caller.  (validate is filled by the caller.)
+    auto t0 = Clock::now();
     const uint32_t entries = n_lists ? first[n_lists] : 0u;
     const bool inl = src.total <= kInlineArena;
     // Large arenas first: their chunks DMA while the metadata is built.
     HIP_TRY(c, c->d_arena.ensure(inl ? 1 : src.total + kArenaSlack));
     if (!inl)
         if (int rc = h2d_arena(c, src, c->d_arena.as<uint8_t>())) return rc;
+    c->prof[MIRSHA_PROF_PACK] = ms_since(t0);
+    t0 = Clock::now();
     std::vector<uint32_t> order_tmp;
     uint32_t lo_b = UINT32_MAX, hi_b = 0;
     for (uint32_t i = 0; i < n; i++) {
@@ -367,20 +426,27 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
     HIP_TRY(c, c->d_meta.ensure(L.end));
     uint8_t* h = c->h_meta.as<uint8_t>();
     if (n) {
-        memcpy(h + L.off, off, 8ull * n);
-        memcpy(h + L.len, len, 4ull * n);
+        pmemcpy(h + L.off, off, 8ull * n);
+        pmemcpy(h + L.len, len, 4ull * n);
         if (ordered) bucket_order(len, n, reinterpret_cast<uint32_t*>(h + L.order));
     }
-    if (entries) memcpy(h + L.idx, idx, 4ull * entries);
-    if (n_lists) memcpy(h + L.first, first, 4ull * (n_lists + 1));
+    if (entries) pmemcpy(h + L.idx, idx, 4ull * entries);
+    if (n_lists) pmemcpy(h + L.first, first, 4ull * (n_lists + 1));
     if (inl && src.total) fill(src, 0, src.total, h + L.arena);
-    HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.end, hipMemcpyHostToDevice, c->stream));
-    uint8_t* dm = c->d_meta.as<uint8_t>();
-    const uint8_t* d_arena = inl ? dm + L.arena : c->d_arena.as<uint8_t>();
-    // Digests: requests then lists, contiguous (one D2H).
+    c->prof[MIRSHA_PROF_PLAN] = ms_since(t0);
+    t0 = Clock::now();
     const uint64_t out_bytes = 32ull * ((uint64_t)n + n_lists);
+    const bool direct = inl && L.end <= kDirectMax && out_bytes <= kDirectMax && direct_small_enabled();
+    uint8_t* dm = h;  // direct: the kernels read the pinned block itself
+    if (!direct) {
+        HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.end, hipMemcpyHostToDevice, c->stream));
+        dm = c->d_meta.as<uint8_t>();
+    }
+    const uint8_t* d_arena = inl ? dm + L.arena : c->d_arena.as<uint8_t>();
+    // Digests: requests then lists, contiguous (one D2H, or none when direct).
     HIP_TRY(c, c->d_out.ensure(std::max<uint64_t>(out_bytes, 32)));
-    uint8_t* d_req = c->d_out.as<uint8_t>();
+    if (direct) HIP_TRY(c, c->h_outs.ensure(std::max<uint64_t>(out_bytes, 32)));
+    uint8_t* d_req = direct ? c->h_outs.as<uint8_t>() : c->d_out.as<uint8_t>();
     uint8_t* d_lst = d_req + 32ull * n;
     if (n) {
         if (int rc = timed_launch(c, 0, [&] {
@@ -406,15 +472,22 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
     }
     if (out_bytes <= kPinnedOutMax) {
         HIP_TRY(c, c->h_outs.ensure(std::max<uint64_t>(out_bytes, 32)));
-        HIP_TRY(c, hipMemcpyAsync(c->h_outs.p, d_req, out_bytes, hipMemcpyDeviceToHost, c->stream));
+        if (!direct) HIP_TRY(c, hipMemcpyAsync(c->h_outs.p, d_req, out_bytes, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
+        c->prof[MIRSHA_PROF_DEVICE] = ms_since(t0);
+        t0 = Clock::now();
         if (n) memcpy(req_out, c->h_outs.p, 32ull * n);
         if (n_lists) memcpy(list_out, c->h_outs.as<uint8_t>() + 32ull * n, 32ull * n_lists);
     } else {
-        if (n) HIP_TRY(c, hipMemcpyAsync(req_out, d_req, 32ull * n, hipMemcpyDeviceToHost, c->stream));
-        if (n_lists) HIP_TRY(c, hipMemcpyAsync(list_out, d_lst, 32ull * n_lists, hipMemcpyDeviceToHost, c->stream));
+        // Large results: device -> pinned ring chunks -> caller, each chunk's
+        // copy-out overlapping the next chunk's DMA.
         HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (bool& b : c->ring_busy) b = false;
+        c->prof[MIRSHA_PROF_DEVICE] = ms_since(t0);
+        t0 = Clock::now();
+        if (int rc = d2h_split(c, d_req, out_bytes, 32ull * n, req_out, list_out)) return rc;
     }
+    c->prof[MIRSHA_PROF_SCATTER] = ms_since(t0);
     for (bool& b : c->ring_busy) b = false;  // every queued chunk DMA has completed
     return MIRSHA_OK;
 }
@@ -443,9 +516,12 @@ int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uin
 int run_arena_call(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off, const uint32_t* len,
                    uint32_t n, const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint8_t* req_out,
                    uint8_t* list_out) {
+    const auto t0 = Clock::now();
+    for (double& x : c->prof) x = 0.0;
     uint64_t lo = 0, hi = 0, total = 0;
     if (int rc = arena_span(c, arena_len, off, len, n, &lo, &hi)) return rc;
     for (uint32_t i = 0; i < n; i++) total += len[i];
+    c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
     std::vector<uint64_t> roff;
     ArenaSrc src;
     std::vector<const uint8_t*> sp;
@@ -1067,8 +1143,11 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
                        const uint32_t* slice_first, uint32_t n, uint8_t* out) {
     if (!c) return MIRSHA_EINVAL;
     if (n == 0) return MIRSHA_OK;
+    const auto t0 = Clock::now();
+    for (double& x : c->prof) x = 0.0;
     std::vector<uint32_t> len;
     if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
+    c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
     if (int rc = use_device(c)) return rc;
     // One packing pass, by threads, straight into pinned staging (the Go
     // side's single copy), chunk by chunk behind the DMA of the previous one.
