@@ -5,7 +5,7 @@ SHA-256 request, batch, VerifyBatch, epoch-change and checkpoint digests,
 bit-exact with Go crypto/sha256, returned in origin order.  All compute runs in
 hand-written gfx950 HIP kernels behind the C-ABI in include/mirsha.h.
 """
-from . import hashdata, sharding
+from . import eventlog, hashdata, sharding
 from ._lib import MirshaError, MirshaUnavailable
 from .engine import CheckpointChains, Engine, SliceArrays, Ticket, bucket_order, dedup_plan, device_count, hash_batch_multi
 from .processor import (ActionResults, Actions, GpuHash, HashRequest, HashResult, PendingResults, Processor,
@@ -23,6 +23,7 @@ __all__ = [
     "bucket_order",
     "device_count",
     "hash_batch_multi",
+    "eventlog",
     "hashdata",
     "sharding",
     "ActionResults",
