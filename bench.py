@@ -370,15 +370,24 @@ class MixedWorkload:
     and the launch's tail is short messages; --windows: <= 4 GiB origin-order
     windows, one launch each (A/B)."""
 
-    def __init__(self, a, eng, dev, rank):
+    def __init__(self, a, eng, dev, rank, world=1):
         self.a, self.eng = a, eng
         _, n0, _, self.desc = CONFIGS[5]
-        self.n = n = a.requests or n0
+        per_rank = a.requests or n0
         self.seed = SEED_BASE + 5
-        self.first_req = rank * n
-        d_len = torch.empty(n, dtype=torch.int32, device=dev)
-        eng.synth_mixed_lengths_device(self.seed, self.first_req, n, d_len.data_ptr())
+        # One global stream of world x per_rank requests, cut into `world`
+        # contiguous request ranges of equal compression count by the
+        # block-balanced sharder (sharding.shard_ranges with lengths): at
+        # N = 8 that is BASELINE config 5's 10^8-request stream.
+        g = world * per_rank
+        d_all = torch.empty(g, dtype=torch.int32, device=dev)
+        eng.synth_mixed_lengths_device(self.seed, 0, g, d_all.data_ptr())
         eng.sync()
+        lo, hi = sharding.shard_ranges(g, world, 1, d_all.cpu().numpy().view(np.uint32))[rank]
+        self.first_req, self.n = lo, n = hi - lo
+        self.global_requests = g
+        d_len = d_all[lo:hi].clone()
+        del d_all
         self.ln = d_len.cpu().numpy().view(np.uint32)
         self.off = np.zeros(n, dtype=np.uint64)
         np.cumsum(self.ln[:-1], out=self.off[1:])
@@ -451,7 +460,10 @@ class MixedWorkload:
         }
 
     def config_fields(self):
-        return {"requests_per_gpu": self.n, "arena_gb_per_gpu": self.total / 1e9,
+        return {"requests_per_gpu": self.n, "global_requests": self.global_requests,
+                "sharding": "sharding.shard_ranges(global stream, world, lengths): contiguous request ranges "
+                            "of equal compression count, no collective",
+                "first_request_of_rank": self.first_req, "arena_gb_per_gpu": self.total / 1e9,
                 "mean_request_bytes": self.total / self.n, "launches_per_step": len(self.wins),
                 "addressing": "4 GiB windows" if self.a.windows else "one launch, 64-bit per-lane addresses",
                 "compressions_per_step_per_gpu": self.req_blocks}
@@ -645,7 +657,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     eng.set_stream(stream.cuda_stream)
 
-    wl = {5: MixedWorkload, 4: EpochChangeWorkload}.get(a.config, BatchWorkload)(a, eng, dev, rank)
+    if a.config == 5:
+        wl = MixedWorkload(a, eng, dev, rank, world)
+    else:
+        wl = {4: EpochChangeWorkload}.get(a.config, BatchWorkload)(a, eng, dev, rank)
     torch.cuda.synchronize(dev)
 
     # PCIe-inclusive host-API rate (rank 0, N=1 only), measured before the
@@ -713,8 +728,13 @@ def main():
     # quick self-check of the last step against the CPU oracle on a sample
     check_ok = wl.self_check() if rank == 0 else None
 
-    value = wl.digests * world * a.steps / dt
-    gbps = wl.bytes_hashed * world * a.steps / dt / 1e9
+    # Whole-job totals: the sum over ranks (config 5's block-balanced shards
+    # differ in request count per rank).
+    tot = torch.tensor([float(wl.digests), float(wl.bytes_hashed)], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    value = float(tot[0].item()) * a.steps / dt
+    gbps = float(tot[1].item()) * a.steps / dt / 1e9
     ms_per_step_k = ms_k / a.steps  # all launches of the dominant kernel in one step
     achieved_tops = work_blocks * OPS_PER_COMPRESSION / (ms_per_step_k * 1e-3) / 1e12
     hbm_gbs = hbm_bytes / (ms_per_step_k * 1e-3) / 1e9

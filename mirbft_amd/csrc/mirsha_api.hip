@@ -122,6 +122,10 @@ struct mirsha_ctx {
     bool ring_busy[kStageSlots] = {};
     PinnedBuf h_meta, h_outs;
     DevBuf d_meta;
+    // Pipelined staged calls (run_pipelined): H2D and D2H each on their own
+    // stream, so chunk k's digests return while chunk k+1's bytes go in.
+    hipStream_t xin = nullptr, xout = nullptr;
+    std::vector<hipEvent_t> xev;  // per-call events (grow-only pool)
     KernelTimer timers[6];         // msgs, lists, gen, chain, fused, (5: retired)
     AsyncSlot slots[kAsyncSlots];
     uint64_t next_ticket = 1;  // ticket of the next submission
@@ -302,6 +306,12 @@ struct ArenaSrc {
     uint64_t total = 0;
 };
 
+// A boolean knob from the environment ("1" = set), read once per call site.
+bool getenv_flag(const char* name) {
+    const char* e = getenv(name);
+    return e && e[0] == '1';
+}
+
 bool host_pinned(const void* p) {
     hipPointerAttribute_t a;
     if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -393,11 +403,204 @@ struct MetaLayout {
     }
 };
 
-// One synchronous call: n messages (offsets relative to the packed arena) and
-// optionally n_lists digest lists over their digests.  req_out / list_out are
-// the caller's host buffers (n x 32, n_lists x 32).
+// Metadata of n messages into the pinned block: offsets rebased by `shift`,
+// lengths, and whether the block counts differ (a bucket order is needed).
+// One parallel pass.
+bool meta_fill(const uint64_t* off, const uint32_t* len, uint32_t n, uint64_t shift, uint8_t* h, const MetaLayout& L) {
+    std::atomic<uint32_t> lo_b{UINT32_MAX}, hi_b{0};
+    uint64_t* ho = reinterpret_cast<uint64_t*>(h + L.off);
+    uint32_t* hl = reinterpret_cast<uint32_t*>(h + L.len);
+    mirsha::host::parallel_for(n, mirsha::host::threads_for(12ull * n, n), [&](uint32_t a, uint32_t b) {
+        uint32_t lo = UINT32_MAX, hi = 0;
+        for (uint32_t i = a; i < b; i++) {
+            ho[i] = off[i] - shift;
+            hl[i] = len[i];
+            const uint32_t k = host_blocks(len[i]);
+            lo = std::min(lo, k);
+            hi = std::max(hi, k);
+        }
+        uint32_t cur = lo_b.load();
+        while (lo < cur && !lo_b.compare_exchange_weak(cur, lo)) {}
+        cur = hi_b.load();
+        while (hi > cur && !hi_b.compare_exchange_weak(cur, hi)) {}
+    });
+    return n && lo_b.load() != hi_b.load();
+}
+
+hipError_t take_events(mirsha_ctx* c, size_t k) {
+    while (c->xev.size() < k) {
+        hipEvent_t e = nullptr;
+        hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (r != hipSuccess) return r;
+        c->xev.push_back(e);
+    }
+    return hipSuccess;
+}
+
+// The pipelined form of a large synchronous call (messages packed in order
+// in [0, total)).  The arena goes over PCIe in kStageChunk chunks on the xin
+// stream (straight from a page-locked caller arena, else packed by the host
+// pool into the pinned ring behind the previous chunks' DMA); as soon as a
+// chunk has landed, the request kernel hashes every message that lies wholly
+// inside the bytes received so far, and the xout stream brings those digests
+// back while the next chunks are still coming in (PCIe is full duplex).  The
+// lists kernel follows the last request chunk.  A call then costs about its
+// H2D time plus one chunk's kernel and D2H, instead of H2D + kernels + D2H +
+// host copy-out in sequence.
+int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const uint32_t* len, uint32_t n,
+                  uint64_t shift, const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint8_t* req_out,
+                  uint8_t* list_out) {
+    double t_pack = 0.0, t_wait = 0.0, t_out = 0.0;
+    const uint64_t total = src.total;
+    const uint32_t entries = n_lists ? first[n_lists] : 0u;
+    const uint32_t nch = (uint32_t)((total + kStageChunk - 1) / kStageChunk);
+    if (!c->xin) HIP_TRY(c, hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
+    if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
+    // events: in[k], kern[k], out[k] per chunk; meta; lists kernel; lists out
+    HIP_TRY(c, take_events(c, 3ull * nch + 3));
+    hipEvent_t* ev_in = c->xev.data();
+    hipEvent_t* ev_kern = ev_in + nch;
+    hipEvent_t* ev_out = ev_kern + nch;
+    hipEvent_t ev_meta = ev_out[nch], ev_lk = ev_out[nch + 1], ev_lo = ev_out[nch + 2];
+    HIP_TRY(c, c->d_arena.ensure(total + kArenaSlack));
+    uint8_t* d_arena = c->d_arena.as<uint8_t>();
+    const bool pinned_src = src.base && host_pinned(src.base);
+    auto queue_in = [&](uint32_t k) -> int {
+        const uint64_t a = (uint64_t)k * kStageChunk, b = std::min(total, a + kStageChunk);
+        const uint8_t* from = pinned_src ? src.base + a : nullptr;
+        if (!from) {
+            const int slot = (int)(k % kStageSlots);
+            if (k >= (uint32_t)kStageSlots) {  // the slot's previous chunk must have left it
+                const auto w = Clock::now();
+                HIP_TRY(c, hipEventSynchronize(ev_in[k - kStageSlots]));
+                t_wait += ms_since(w);
+            }
+            HIP_TRY(c, c->h_ring[slot].ensure(kStageChunk));
+            const auto p = Clock::now();
+            fill(src, a, b, c->h_ring[slot].as<uint8_t>());
+            t_pack += ms_since(p);
+            from = c->h_ring[slot].as<uint8_t>();
+        }
+        HIP_TRY(c, hipMemcpyAsync(d_arena + a, from, b - a, hipMemcpyHostToDevice, c->xin));
+        HIP_TRY(c, hipEventRecord(ev_in[k], c->xin));
+        return MIRSHA_OK;
+    };
+    if (int rc = queue_in(0)) return rc;
+
+    // Metadata (behind chunk 0 on the same copy stream).  Chunk k hashes the
+    // messages [cut[k], cut[k+1]): those ending within its first B_k bytes.
+    const auto tp = Clock::now();
+    std::vector<uint32_t> cut(nch + 1, 0);
+    for (uint32_t k = 0; k + 1 < nch; k++) {
+        const uint64_t bk = (uint64_t)(k + 1) * kStageChunk;
+        uint32_t lo = cut[k], hi = n;  // first i with end(i) > bk (ends are nondecreasing)
+        while (lo < hi) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (off[mid] - shift + len[mid] <= bk) lo = mid + 1; else hi = mid;
+        }
+        cut[k + 1] = lo;
+    }
+    cut[nch] = n;
+    MetaLayout L(n, true, entries, n_lists, 0);
+    HIP_TRY(c, c->h_meta.ensure(L.end));
+    HIP_TRY(c, c->d_meta.ensure(L.end));
+    uint8_t* h = c->h_meta.as<uint8_t>();
+    const bool ordered = meta_fill(off, len, n, shift, h, L);
+    if (ordered) {  // a bucket order per chunk, indices local to the chunk
+        mirsha::host::parallel_for(nch, (int)nch, [&](uint32_t a, uint32_t b) {
+            for (uint32_t k = a; k < b; k++)
+                bucket_order(len + cut[k], cut[k + 1] - cut[k], reinterpret_cast<uint32_t*>(h + L.order) + cut[k]);
+        });
+    }
+    if (entries) pmemcpy(h + L.idx, idx, 4ull * entries);
+    if (n_lists) pmemcpy(h + L.first, first, 4ull * (n_lists + 1));
+    HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.end, hipMemcpyHostToDevice, c->xin));
+    HIP_TRY(c, hipEventRecord(ev_meta, c->xin));
+    HIP_TRY(c, hipStreamWaitEvent(c->stream, ev_meta, 0));
+    c->prof[MIRSHA_PROF_PLAN] = ms_since(tp);
+    uint8_t* dm = c->d_meta.as<uint8_t>();
+
+    const uint64_t out_bytes = 32ull * ((uint64_t)n + n_lists);
+    HIP_TRY(c, c->d_out.ensure(std::max<uint64_t>(out_bytes, 32)));
+    uint8_t* d_req = c->d_out.as<uint8_t>();
+    uint8_t* d_lst = d_req + 32ull * n;
+    const bool direct_out = host_pinned(req_out);
+    HIP_TRY(c, c->h_outs.ensure(std::max<uint64_t>(direct_out ? 32ull * n_lists : out_bytes, 32)));
+    uint8_t* h_req = direct_out ? req_out : c->h_outs.as<uint8_t>();
+    uint8_t* h_lst = direct_out ? c->h_outs.as<uint8_t>() : h_req + 32ull * n;
+
+    uint32_t copied = 0;  // chunks whose digests are in req_out
+    auto copy_out = [&](uint32_t k) {
+        if (!direct_out && cut[k + 1] > cut[k]) {
+            const auto w = Clock::now();
+            pmemcpy(req_out + 32ull * cut[k], h_req + 32ull * cut[k], 32ull * (cut[k + 1] - cut[k]));
+            t_out += ms_since(w);
+        }
+    };
+    for (uint32_t k = 0; k < nch; k++) {
+        if (k > 0)
+            if (int rc = queue_in(k)) return rc;
+        const uint32_t i0 = cut[k], cnt = cut[k + 1] - i0;
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, ev_in[k], 0));
+        if (cnt) {
+            if (int rc = timed_launch(c, 0, [&] {
+                    return mirsha::launch_msgs(d_arena, total, reinterpret_cast<const uint64_t*>(dm + L.off) + i0,
+                                               reinterpret_cast<const uint32_t*>(dm + L.len) + i0,
+                                               ordered ? reinterpret_cast<const uint32_t*>(dm + L.order) + i0 : nullptr,
+                                               cnt, d_req + 32ull * i0, c->variant, c->stream);
+                }))
+                return rc;
+        }
+        HIP_TRY(c, hipEventRecord(ev_kern[k], c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->xout, ev_kern[k], 0));
+        if (cnt) HIP_TRY(c, hipMemcpyAsync(h_req + 32ull * i0, d_req + 32ull * i0, 32ull * cnt, hipMemcpyDeviceToHost, c->xout));
+        HIP_TRY(c, hipEventRecord(ev_out[k], c->xout));
+        // digests that are already back go to the caller while later chunks pack
+        while (copied < k && hipEventQuery(ev_out[copied]) == hipSuccess) copy_out(copied++);
+    }
+    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
+    if (n_lists) {
+        HIP_TRY(c, c->d_scratch.ensure(sizeof(uint32_t) * std::max<uint32_t>(entries, 1)));
+        if (int rc = timed_launch(c, 1, [&] {
+                return mirsha::launch_lists(d_req, n, reinterpret_cast<const uint32_t*>(dm + L.idx), entries,
+                                            reinterpret_cast<const uint32_t*>(dm + L.first), n_lists,
+                                            c->d_scratch.as<uint32_t>(), d_lst, c->stream);
+            }))
+            return rc;
+        HIP_TRY(c, hipEventRecord(ev_lk, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->xout, ev_lk, 0));
+        HIP_TRY(c, hipMemcpyAsync(h_lst, d_lst, 32ull * n_lists, hipMemcpyDeviceToHost, c->xout));
+        HIP_TRY(c, hipEventRecord(ev_lo, c->xout));
+    }
+    for (; copied < nch; copied++) {
+        const auto w = Clock::now();
+        HIP_TRY(c, hipEventSynchronize(ev_out[copied]));
+        t_wait += ms_since(w);
+        copy_out(copied);
+    }
+    if (n_lists) {
+        const auto w = Clock::now();
+        HIP_TRY(c, hipEventSynchronize(ev_lo));
+        t_wait += ms_since(w);
+        memcpy(list_out, h_lst, 32ull * n_lists);
+    }
+    // The caller's stream also saw every kernel finish (ev_out waits on them).
+    c->prof[MIRSHA_PROF_PACK] = t_pack;
+    c->prof[MIRSHA_PROF_DEVICE] = t_wait;
+    c->prof[MIRSHA_PROF_SCATTER] = t_out;
+    return MIRSHA_OK;
+}
+
+// One synchronous call: n messages (offsets minus `shift` are positions in the
+// packed arena) and optionally n_lists digest lists over their digests.
+// req_out / list_out are the caller's host buffers (n x 32, n_lists x 32).
+// `inorder`: the messages lie in [0, total) back to back in index order (each
+// starts at or after the previous one's end), which the pipelined form needs.
 int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const uint32_t* len, uint32_t n,
-               const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint8_t* req_out, uint8_t* list_out) {
+               uint64_t shift, bool inorder, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
+               uint8_t* req_out, uint8_t* list_out) {
+    if (n && inorder && src.total > kStageChunk && !getenv_flag("MIRSHA_NO_PIPELINED_CALLS"))
+        return run_pipelined(c, src, off, len, n, shift, idx, first, n_lists, req_out, list_out);
     // Host phases into c->prof (mirsha_ctx_host_profile): pack = queueing the
     // request bytes, plan = metadata block, device = queue -> sync, scatter =
     // digests to the caller.  (validate is filled by the caller.)
@@ -410,23 +613,12 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
         if (int rc = h2d_arena(c, src, c->d_arena.as<uint8_t>())) return rc;
     c->prof[MIRSHA_PROF_PACK] = ms_since(t0);
     t0 = Clock::now();
-    std::vector<uint32_t> order_tmp;
-    uint32_t lo_b = UINT32_MAX, hi_b = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t b = host_blocks(len[i]);
-        lo_b = std::min(lo_b, b);
-        hi_b = std::max(hi_b, b);
-    }
-    const bool ordered = n && lo_b != hi_b;
-    const MetaLayout L(n, ordered, entries, n_lists, inl ? src.total : 0);
+    const MetaLayout L(n, true, entries, n_lists, inl ? src.total : 0);
     HIP_TRY(c, c->h_meta.ensure(L.end));
     HIP_TRY(c, c->d_meta.ensure(L.end));
     uint8_t* h = c->h_meta.as<uint8_t>();
-    if (n) {
-        pmemcpy(h + L.off, off, 8ull * n);
-        pmemcpy(h + L.len, len, 4ull * n);
-        if (ordered) bucket_order(len, n, reinterpret_cast<uint32_t*>(h + L.order));
-    }
+    const bool ordered = meta_fill(off, len, n, shift, h, L);
+    if (ordered) bucket_order(len, n, reinterpret_cast<uint32_t*>(h + L.order));
     if (entries) pmemcpy(h + L.idx, idx, 4ull * entries);
     if (n_lists) pmemcpy(h + L.first, first, 4ull * (n_lists + 1));
     if (inl && src.total) fill(src, 0, src.total, h + L.arena);
@@ -487,18 +679,21 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
     return MIRSHA_OK;
 }
 
-// Validates messages of a caller arena; rebases them on the smallest offset.
-// Returns the dense span [lo, hi) or fails.
+// Validates messages of a caller arena: the dense span [lo, hi) they cover,
+// their total length, and whether they lie back to back in index order
+// (off[i] >= off[i-1] + len[i-1]).  One parallel pass.
 int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uint32_t* len, uint32_t n,
-               uint64_t* lo_out, uint64_t* hi_out) {
+               uint64_t* lo_out, uint64_t* hi_out, uint64_t* total_out = nullptr, bool* inorder_out = nullptr) {
     // Threads over index ranges; the first bad message (lowest index) is reported.
     const int T = mirsha::host::threads_for(12ull * n, n);
-    std::vector<uint64_t> los(T, UINT64_MAX), his(T, 0);
+    std::vector<uint64_t> los(T, UINT64_MAX), his(T, 0), tot(T, 0);
     std::vector<uint32_t> bad(T, UINT32_MAX);
-    std::atomic<int> part{0};
+    std::vector<uint8_t> ord(T, 1);
+    const uint32_t step = (n + T - 1) / std::max(T, 1);
     mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
-        const int k = part.fetch_add(1);
-        uint64_t lo = UINT64_MAX, hi = 0;
+        const int k = (int)(a / std::max<uint32_t>(step, 1));
+        uint64_t lo = UINT64_MAX, hi = 0, t = 0;
+        bool in = true;
         for (uint32_t i = a; i < b; i++) {
             if (len[i] > MIRSHA_MAX_MESSAGE_BYTES || off[i] > arena_len || len[i] > arena_len - off[i]) {
                 bad[k] = i;
@@ -506,9 +701,13 @@ int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uin
             }
             lo = std::min<uint64_t>(lo, off[i]);
             hi = std::max<uint64_t>(hi, off[i] + len[i]);
+            t += len[i];
+            if (i && off[i] < off[i - 1] + len[i - 1]) in = false;
         }
         los[k] = lo;
         his[k] = hi;
+        tot[k] = t;
+        ord[k] = in;
     });
     const uint32_t i = *std::min_element(bad.begin(), bad.end());
     if (i != UINT32_MAX) {
@@ -519,6 +718,10 @@ int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uin
     }
     *lo_out = n ? *std::min_element(los.begin(), los.end()) : 0;
     *hi_out = n ? *std::max_element(his.begin(), his.end()) : 0;
+    uint64_t t = 0;
+    for (uint64_t x : tot) t += x;
+    if (total_out) *total_out = t;
+    if (inorder_out) *inorder_out = std::all_of(ord.begin(), ord.end(), [](uint8_t x) { return x != 0; });
     return MIRSHA_OK;
 }
 
@@ -530,42 +733,36 @@ int run_arena_call(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, cons
     const auto t0 = Clock::now();
     for (double& x : c->prof) x = 0.0;
     uint64_t lo = 0, hi = 0, total = 0;
-    if (int rc = arena_span(c, arena_len, off, len, n, &lo, &hi)) return rc;
-    for (uint32_t i = 0; i < n; i++) total += len[i];
+    bool inorder = false;
+    if (int rc = arena_span(c, arena_len, off, len, n, &lo, &hi, &total, &inorder)) return rc;
     c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
-    std::vector<uint64_t> roff;
     ArenaSrc src;
-    std::vector<const uint8_t*> sp;
-    std::vector<uint64_t> sl;
-    std::vector<uint32_t> sf;
-    if (hi - lo <= 2 * total + 4096) {  // dense: ship the span, offsets rebased
+    if (hi - lo <= 2 * total + 4096) {  // dense: ship the span, offsets rebased on lo
         src.base = arena + lo;
         src.total = hi - lo;
-        if (lo == 0) return run_staged(c, src, off, len, n, idx, first, n_lists, req_out, list_out);
-        roff.resize(n);
-        for (uint32_t i = 0; i < n; i++) roff[i] = off[i] - lo;
-    } else {  // sparse: one slice per message, packed
-        roff.resize(n);
-        sp.resize(n);
-        sl.resize(n);
-        sf.resize(n + 1);
-        uint64_t p = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            sp[i] = arena + off[i];
-            sl[i] = len[i];
-            sf[i] = i;
-            roff[i] = p;
-            p += len[i];
-        }
-        sf[n] = n;
-        src.ptr = sp.data();
-        src.slen = sl.data();
-        src.sfirst = sf.data();
-        src.poff = roff.data();
-        src.n = n;
-        src.total = total;
+        return run_staged(c, src, off, len, n, lo, inorder, idx, first, n_lists, req_out, list_out);
     }
-    return run_staged(c, src, roff.data(), len, n, idx, first, n_lists, req_out, list_out);
+    // sparse: one slice per message, packed back to back
+    std::vector<uint64_t> roff(n);
+    std::vector<const uint8_t*> sp(n);
+    std::vector<uint64_t> sl(n);
+    std::vector<uint32_t> sf(n + 1);
+    uint64_t p = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        sp[i] = arena + off[i];
+        sl[i] = len[i];
+        sf[i] = i;
+        roff[i] = p;
+        p += len[i];
+    }
+    sf[n] = n;
+    src.ptr = sp.data();
+    src.slen = sl.data();
+    src.sfirst = sf.data();
+    src.poff = roff.data();
+    src.n = n;
+    src.total = total;
+    return run_staged(c, src, roff.data(), len, n, 0, true, idx, first, n_lists, req_out, list_out);
 }
 
 // ---- request -> batch-digest plan (sequential form) ------------------------
@@ -1067,6 +1264,9 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     c->h_meta.release();
     c->h_outs.release();
     c->d_meta.release();
+    for (auto e : c->xev) (void)hipEventDestroy(e);
+    if (c->xin) (void)hipStreamDestroy(c->xin);
+    if (c->xout) (void)hipStreamDestroy(c->xout);
     for (auto& sl : c->slots) {
         sl.stage.release(); sl.dig.release(); sl.dev.release();
         if (sl.done) (void)hipEventDestroy(sl.done);
@@ -1175,7 +1375,7 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
     src.poff = poff.data();
     src.n = n;
     src.total = p;
-    return run_staged(c, src, poff.data(), len.data(), n, nullptr, nullptr, 0, out, nullptr);
+    return run_staged(c, src, poff.data(), len.data(), n, 0, true, nullptr, nullptr, 0, out, nullptr);
 }
 
 int mirsha_host_alloc(mirsha_ctx* c, uint64_t bytes, void** out) {
@@ -1291,7 +1491,7 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
     if (n_req == 0 && n_batches == 0) return MIRSHA_OK;
     if (n_req == 0) {  // lists of null requests only (every entry is MIRSHA_NULL_INDEX)
         ArenaSrc none;
-        return run_staged(c, none, nullptr, nullptr, 0, idx, first, n_batches, nullptr, batch_out);
+        return run_staged(c, none, nullptr, nullptr, 0, 0, false, idx, first, n_batches, nullptr, batch_out);
     }
     return run_arena_call(c, arena, arena_len, off, len, n_req, idx, first, n_batches, req_out, batch_out);
 }
@@ -1382,7 +1582,7 @@ int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digest
     ArenaSrc src;  // the digests themselves are the arena the lists index
     src.base = digests;
     src.total = 32ull * n_digests;
-    return run_staged(c, src, nullptr, nullptr, 0, idx, first, n_lists, nullptr, out);
+    return run_staged(c, src, nullptr, nullptr, 0, 0, false, idx, first, n_lists, nullptr, out);
 }
 
 int mirsha_hash_batch_device(mirsha_ctx* c, const uint8_t* d_arena, uint64_t arena_len,

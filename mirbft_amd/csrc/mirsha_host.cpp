@@ -7,6 +7,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -99,13 +102,94 @@ struct Fp {
 
 }  // namespace
 
+namespace {
+
+// Persistent workers for parallel_for.  A staged host call runs a dozen
+// parallel passes (validation, metadata, one pack per pinned chunk, digest
+// copy-out); spawning and joining 16 std::threads per pass cost ~0.1-0.3 ms
+// each, which was most of the validate / plan phases of a config-2 call.
+// One job at a time (callers serialise on `submit_`); the calling thread takes
+// parts too.  A parallel_for issued from inside a job runs inline.  The pool
+// is created on first use and never destroyed (workers park on a condition
+// variable until the process exits).
+thread_local bool t_in_pool_job = false;
+
+class Pool {
+  public:
+    explicit Pool(int workers) {
+        for (int w = 0; w < workers; w++) std::thread([this] { loop(); }).detach();
+    }
+    void run(uint32_t n, int parts, const std::function<void(uint32_t, uint32_t)>& fn) {
+        std::lock_guard<std::mutex> one(submit_);
+        {
+            std::lock_guard<std::mutex> g(m_);
+            fn_ = &fn;
+            n_ = n;
+            parts_ = parts;
+            step_ = (n + parts - 1) / parts;
+            next_.store(0);
+            left_ = parts;
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> g(m_);
+        done_.wait(g, [this] { return left_ == 0; });
+        fn_ = nullptr;
+    }
+
+  private:
+    void work() {
+        const bool was = t_in_pool_job;
+        t_in_pool_job = true;
+        for (;;) {
+            const int p = next_.fetch_add(1);
+            if (p >= parts_) break;
+            const uint32_t lo = (uint32_t)std::min<uint64_t>((uint64_t)p * step_, n_);
+            const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)(p + 1) * step_, n_);
+            if (lo < hi) (*fn_)(lo, hi);
+            std::lock_guard<std::mutex> g(m_);
+            if (--left_ == 0) done_.notify_all();
+        }
+        t_in_pool_job = was;
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (!fn_) continue;
+            }
+            work();
+        }
+    }
+    std::mutex submit_, m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(uint32_t, uint32_t)>* fn_ = nullptr;
+    uint32_t n_ = 0, step_ = 0;
+    int parts_ = 0, left_ = 0;
+    std::atomic<int> next_{0};
+    uint64_t gen_ = 0;
+};
+
+int max_threads() {
+    int t = env_threads();
+    if (t <= 0) t = std::min(std::max((int)std::thread::hardware_concurrency(), 1), 16);
+    return t;
+}
+
+Pool& pool() {
+    static Pool* p = new Pool(max_threads() - 1);
+    return *p;
+}
+
+}  // namespace
+
 int threads_for(uint64_t bytes, uint32_t n) {
     if (n < 2 || bytes < (4ull << 20)) return 1;
-    int t = env_threads();
-    if (t <= 0) {
-        t = (int)std::thread::hardware_concurrency();
-        t = std::min(std::max(t, 1), 16);
-    }
+    int t = max_threads();
     const uint64_t by_bytes = bytes / (1ull << 20);  // >= 1 MiB per thread
     t = (int)std::min<uint64_t>((uint64_t)t, std::max<uint64_t>(1, by_bytes));
     return std::min<int>(t, (int)n);
@@ -113,19 +197,12 @@ int threads_for(uint64_t bytes, uint32_t n) {
 
 void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, uint32_t)>& fn) {
     if (n == 0) return;
-    if (threads <= 1) {
+    threads = std::min<int>(threads, (int)n);
+    if (threads <= 1 || t_in_pool_job) {
         fn(0, n);
         return;
     }
-    std::vector<std::thread> pool;
-    pool.reserve(threads - 1);
-    const uint32_t step = (n + threads - 1) / threads;
-    for (int t = 1; t < threads; t++) {
-        const uint32_t lo = std::min<uint64_t>((uint64_t)t * step, n), hi = std::min<uint64_t>((uint64_t)(t + 1) * step, n);
-        if (lo < hi) pool.emplace_back([&fn, lo, hi] { fn(lo, hi); });
-    }
-    fn(0, std::min(step, n));
-    for (auto& th : pool) th.join();
+    pool().run(n, threads, fn);
 }
 
 uint64_t fingerprint(const uint8_t* const* ptr, const uint64_t* len, uint32_t s0, uint32_t s1) {

@@ -68,3 +68,52 @@ def test_sharded_gather_equals_single_process(world):
     for rank, req, bat in results:
         assert req == want_req.tobytes(), rank
         assert bat == want_bat.tobytes(), rank
+
+
+SEED5 = synth.SEED_BASE + 5
+
+
+def _rank_mixed(rank, world, port, n, q):
+    """Config 5's form: one global mixed-length stream, block-balanced shards."""
+    import torch.distributed as dist
+
+    from mirbft_amd.dist import hash_sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lengths = np.array([oracle_py.mixed_data_len(SEED5, i) + 16 for i in range(n)], dtype=np.uint32)
+
+    def hash_fn(lo, hi):
+        arena, off, ln = oracle_py.gen_mixed(SEED5, np.arange(lo, hi, dtype=np.uint64))
+        assert np.array_equal(ln, lengths[lo:hi])
+        return oracle_py.hash_requests(arena, off, ln), np.zeros((0, 32), np.uint8)
+
+    req, _ = hash_sharded(hash_fn, n, 1, lengths)
+    q.put((rank, req.tobytes(), sharding.shard_ranges(n, world, 1, lengths)[rank]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_block_balanced_mixed_stream(world):
+    n = 600
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_mixed, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    arena, off, ln = oracle_py.gen_mixed(SEED5, np.arange(n, dtype=np.uint64))
+    want = oracle_py.hash_requests(arena, off, ln)
+    blk = sharding.blocks_for_len(ln).astype(np.int64)
+    shares = []
+    for rank, req, (lo, hi) in results:
+        assert req == want.tobytes(), rank
+        shares.append(int(blk[lo:hi].sum()))
+    # every shard within one request's compressions of the fair share
+    assert max(shares) - min(shares) <= 2 * int(blk.max()), shares
