@@ -140,6 +140,26 @@ __device__ __forceinline__ void pad_words(uint32_t p, uint32_t L, bool last_bloc
     }
 }
 
+// The same padding for a whole block of 16 words when the block position
+// soff, the length L and `last` are wave-uniform (SGPRs): the keep / mark
+// words are scalar, one v_bitop3 per word.
+__device__ __forceinline__ void pad_block_uniform(uint32_t w[16], uint32_t soff, uint32_t L, bool last) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int32_t t = (int32_t)(L - (soff + 4u * k));  // message bytes left at word k
+        const uint32_t sh = (uint32_t)t << 3;              // only used when 0 <= t <= 3
+        uint32_t keep = t >= 4 ? 0xFFFFFFFFu : (t <= 0 ? 0u : ~(0xFFFFFFFFu >> sh));
+        uint32_t mark = (t >= 0 && t < 4) ? 0x80000000u >> sh : 0u;
+        if (k >= 14 && last) {  // 64-bit big-endian bit length
+            keep = 0u;
+            mark = k == 14 ? L >> 29 : L << 3;
+        }
+        keep = __builtin_amdgcn_readfirstlane(keep);
+        mark = __builtin_amdgcn_readfirstlane(mark);
+        w[k] = (w[k] & keep) | mark;
+    }
+}
+
 __device__ __forceinline__ void finish_chunk(const RawChunk& c, uint32_t p, uint32_t L, bool last_block,
                                              uint32_t q, uint32_t out[4]) {
 #pragma unroll
@@ -219,7 +239,6 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
                                           uint4* my, uint32_t t, uint32_t lane) {
-    MIRSHA_STAMP(t, 0);
     // Prologue at the highest issue priority, back to 0 at the first
     // compression: a fresh wave is the youngest on its SIMD and at the default
     // priority gets the VALU only when every older wave stalls, so its
@@ -227,6 +246,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     // (tools/stamp_run.py).  Same-box A/B (profiles/r02h): 196.4 us per
     // config-2 launch vs 201.9 us without.
 #ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 prologue (conditional loads, default priority)
+    MIRSHA_STAMP(t, 0);
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
@@ -236,6 +256,9 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #ifndef MIRSHA_AB_NOPRIO  // A/B build only: default-priority prologue
     __builtin_amdgcn_s_setprio(3);
 #endif
+    // (after the priority raise: the stamp's own VALU at priority 0 starved
+    // for ~29 us in second-generation waves, profiles/r02m)
+    MIRSHA_STAMP(t, 0);
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     // Unconditional loads (n >= 1; an idle lane reads the last message's
@@ -291,6 +314,17 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         // a VGPR compare it became an exec-mask branch with the word assembly
         // duplicated).
         const uint32_t min_l = wave_min(valid ? L : 0xFFFFFFFFu);
+        // Every valid message of the tile the same length (wave-uniform; the
+        // common case: BASELINE configs 2 and 3, batch digest lists): the FIPS
+        // padding words of a block are then the same for every lane, so they
+        // are applied once per lane AFTER the LDS transpose, with the masks
+        // computed on the scalar unit (16 VALU per padded block instead of the
+        // per-chunk form's ~128 on the loader side).
+#ifdef MIRSHA_AB_PRODUCER_PAD  // A/B build only: loader-side padding for every tile
+        const bool uni = false;
+#else
+        const bool uni = wave_max(valid ? L : 0u) == min_l;
+#endif
         uint32_t vo[4], sel[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -299,9 +333,36 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             sel[j] = be_sel(a & 3u);
         }
         MIRSHA_STAMP(t, 1);
+#ifdef MIRSHA_AB_PREFETCH  // A/B build only: next block's chunks in registers (6 waves/SIMD)
+        const bool pf = far && aligned;
+        uint32_t nx[4][4];
+        if (pf) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], 0, 0);
+                nx[j][0] = v[0]; nx[j][1] = v[1]; nx[j][2] = v[2]; nx[j][3] = v[3];
+            }
+        }
+#endif
         for (uint32_t blk = 0; blk < wave_nb; blk++) {
             const uint32_t soff = 64u * blk;
             RawChunk rc[4];
+#ifdef MIRSHA_AB_PREFETCH
+            if (pf) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    rc[j].v[0] = nx[j][0]; rc[j].v[1] = nx[j][1]; rc[j].v[2] = nx[j][2]; rc[j].v[3] = nx[j][3];
+                    rc[j].v[4] = 0u;
+                }
+                if (blk + 1u < wave_nb) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], soff + 64u, 0);
+                        nx[j][0] = v[0]; nx[j][1] = v[1]; nx[j][2] = v[2]; nx[j][3] = v[3];
+                    }
+                }
+            } else
+#endif
             if (far) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -324,7 +385,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                 uint32_t wq[4];
 #pragma unroll
                 for (int k = 0; k < 4; k++) wq[k] = be_word(rc[j].v[k + 1], rc[j].v[k], sel[j]);
-                if (pad) {
+                if (pad && !uni) {
                     // Lengths fetched here (rare blocks), not kept live across the rounds.
                     const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(lane >> 2), 64);
                     pad_words(soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
@@ -346,6 +407,13 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (pad && uni) {
+                // (through an opaque s_mov: hipcc otherwise peels the loop's
+                // last iteration to fold the test, a third copy of the rounds)
+                uint32_t left;
+                asm volatile("s_sub_u32 %0, %1, %2" : "=s"(left) : "s"(wave_nb), "s"(blk));
+                pad_block_uniform(w, soff, min_l, left == 1u);
+            }
 #ifndef MIRSHA_AB_NOPRIO
             if (blk == 0u) __builtin_amdgcn_s_setprio(0);
 #endif
@@ -423,12 +491,19 @@ constexpr uint32_t kMsgWaves = 4;
 #else
 constexpr uint32_t kMsgWaves = 1;
 #endif
+#if defined(MIRSHA_AB_PREFETCH)  // A/B build only: 5 waves/SIMD (up to 96 VGPRs)
+constexpr uint32_t kMsgOcc = 5, kTileSlots = 256;
+#elif defined(MIRSHA_AB_OCC6)  // A/B build only: 6 waves/SIMD
+constexpr uint32_t kMsgOcc = 6, kTileSlots = 416;  // 6.5 KiB LDS per wave: 24 waves per CU
+#else
+constexpr uint32_t kMsgOcc = 8, kTileSlots = 256;
+#endif
 template <bool kLds, bool kWide = false>
-__global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : 8) void sha256_msgs_kernel(
+__global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_msgs_kernel(
     const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
     const uint32_t* __restrict__ len, const uint32_t* __restrict__ order, uint32_t n,
     uint8_t* __restrict__ out) {
-    __shared__ uint4 tile[kMsgWaves][256];
+    __shared__ uint4 tile[kMsgWaves][kTileSlots];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * kMsgWaves + wv;

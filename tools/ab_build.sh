@@ -8,6 +8,9 @@
 #   noprio:    -DMIRSHA_AB_NOPRIO       (request prologue at the default issue priority)
 #   wg4:       -DMIRSHA_AB_WG4          (4-wave request workgroups)
 #   stamps:    -DMIRSHA_AB_STAMPS       (per-tile timeline for tools/stamp_run.py)
+#   ppad:      -DMIRSHA_AB_PRODUCER_PAD (loader-side padding for uniform-length tiles too)
+#   occ6:      -DMIRSHA_AB_OCC6         (request kernel held to 6 waves/SIMD by LDS)
+#   pf5:       -DMIRSHA_AB_PREFETCH     (next block chunks prefetched into registers, 5 waves/SIMD)
 set -euo pipefail
 cd "$(dirname "$0")/.."
 SRC=mirbft_amd/csrc
@@ -22,5 +25,8 @@ build oldpro -DMIRSHA_AB_OLDPROLOGUE &
 build noprio -DMIRSHA_AB_NOPRIO &
 build wg4 -DMIRSHA_AB_WG4 &
 build stamps -DMIRSHA_AB_STAMPS &
+build ppad -DMIRSHA_AB_PRODUCER_PAD &
+build occ6 -DMIRSHA_AB_OCC6 &
+build pf5 -DMIRSHA_AB_PREFETCH &
 wait
 ls -la tools/scratch/*/libmirsha.so
