@@ -270,23 +270,26 @@ class BatchWorkload:
                                                     batch_out=bat_h)
 
             call()  # warm device buffers
-            reps, t1 = 5, time.perf_counter()
-            for _ in range(reps):
+            t = []
+            for _ in range(10):
+                t1 = time.perf_counter()
                 call()
-            return (time.perf_counter() - t1) / reps
+                t.append(time.perf_counter() - t1)
+            return float(np.median(t)), [round(x * 1e3, 3) for x in t]
 
-        pdt = rate(arena_h)
+        pdt, pcalls = rate(arena_h)
         pprof = self.eng.host_profile()
         pinned = self.eng.host_empty(arena_h.size)
         pinned[:] = arena_h
-        qdt = rate(pinned)
+        qdt, qcalls = rate(pinned)
         qprof = self.eng.host_profile()
         self.eng.set_stream(torch.cuda.current_stream(self.d_arena.device).cuda_stream)  # back to the steps' stream
         return {"digests_per_s": self.digests / pdt, "gb_per_s": self.bytes_hashed / pdt / 1e9,
-                "ms_per_call": pdt * 1e3, "host_phases_ms": pprof,
-                "note": "host API (pageable arena -> HBM -> digests -> reused host buffers), synchronous",
+                "ms_per_call": pdt * 1e3, "calls_ms": pcalls, "host_phases_ms": pprof,
+                "note": "host API (pageable arena -> HBM -> digests -> reused host buffers), synchronous; "
+                        "median of 10 calls after one warm-up call; host_phases_ms = the last call's phases",
                 "pinned_arena": {"digests_per_s": self.digests / qdt, "gb_per_s": self.bytes_hashed / qdt / 1e9,
-                                 "ms_per_call": qdt * 1e3, "host_phases_ms": qprof,
+                                 "ms_per_call": qdt * 1e3, "calls_ms": qcalls, "host_phases_ms": qprof,
                                  "note": "the same call on an arena from mirsha_host_alloc (page-locked)"}}
 
     def cpu_baseline(self, seconds):

@@ -177,14 +177,18 @@ int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
  * mirsha_digest_lists): validate = arguments; pack = queueing the request
  * bytes (pinned arena: one DMA; else packing into pinned chunks behind their
  * DMA); plan = the metadata block; device = queue -> synchronised; scatter =
- * digests to the caller.  Writes min(n, phases) entries; returns the number
- * of phases. */
+ * digests to the caller.  Large synchronous calls are pipelined (chunked
+ * H2D, kernels and D2H overlap): there pack = host time spent packing, device
+ * = host time spent waiting on the device, scatter = copying digests out, and
+ * the phases overlap the DMA rather than add up.  total = the whole call.
+ * Writes min(n, phases) entries; returns the number of phases. */
 #define MIRSHA_PROF_VALIDATE 0
 #define MIRSHA_PROF_PLAN 1
 #define MIRSHA_PROF_PACK 2
 #define MIRSHA_PROF_DEVICE 3
 #define MIRSHA_PROF_SCATTER 4
-#define MIRSHA_PROF_PHASES 5
+#define MIRSHA_PROF_TOTAL 5
+#define MIRSHA_PROF_PHASES 6
 int mirsha_ctx_host_profile(const mirsha_ctx* ctx, double* ms_out, int n);
 
 /* Request digests, then the dependent batch digests computed ON DEVICE from

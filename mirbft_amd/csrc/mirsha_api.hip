@@ -114,6 +114,7 @@ struct mirsha_ctx {
     uint32_t time_mask = 0xFFFFFFFFu;  // kernels timed while timing is on
     std::string err;
     DevBuf d_arena, d_off, d_len, d_order, d_out, d_idx, d_first, d_out2, d_scratch;
+    DevBuf d_scan;  // scratch of the offsets scan (pipelined gapless calls)
     // Staged host calls (see "staged host calls" below): a ring of pinned
     // chunks for pageable request bytes, one pinned metadata block (plus small
     // arenas) -> one H2D, and pinned digest staging for small results.
@@ -321,10 +322,13 @@ bool host_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
-// memcpy by host threads (multi-MB metadata and result copies).
+// memcpy by host threads (metadata and result copies): one thread per
+// 256 KiB (a 3.7 MB chunk of digests got 3 threads at the 1 MiB grain of
+// threads_for, ~25 GB/s, and the copy-out was 1.3 ms of a config-2 call).
 void pmemcpy(void* dst, const void* src, uint64_t n) {
+    const int t = n < (1u << 19) ? 1 : (int)std::min<uint64_t>(mirsha::host::threads_for(1ull << 40, 1u << 20), n >> 18);
     mirsha::host::pack_range(static_cast<const uint8_t*>(src), nullptr, nullptr, nullptr, 0, nullptr, 0, n,
-                             static_cast<uint8_t*>(dst), mirsha::host::threads_for(n, 1u << 20));
+                             static_cast<uint8_t*>(dst), t);
 }
 
 void fill(const ArenaSrc& src, uint64_t a, uint64_t b, uint8_t* dst) {
@@ -447,13 +451,60 @@ hipError_t take_events(mirsha_ctx* c, size_t k) {
 // lists kernel follows the last request chunk.  A call then costs about its
 // H2D time plus one chunk's kernel and D2H, instead of H2D + kernels + D2H +
 // host copy-out in sequence.
+// Per-call metadata of the pipelined path: [len u32 | idx u32 | first u32 |
+// order u32 (if the block counts differ) | off u64].  Only [0, copy) goes over
+// PCIe: off is left out when the requests are gapless (rebuilt on the device
+// by an exclusive scan of len), order when it is not needed.
+struct PipeLayout {
+    uint64_t len, idx, first, order, off, end, copy;
+    PipeLayout(uint32_t n, uint32_t entries, uint32_t n_lists, bool ordered, bool gapless) {
+        auto al = [](uint64_t x) { return (x + 15u) & ~15ull; };
+        len = 0;
+        idx = al(len + 4ull * n);
+        first = al(idx + 4ull * entries);
+        order = al(first + (n_lists ? 4ull * (n_lists + 1) : 0));
+        off = al(order + (ordered ? 4ull * n : 0));
+        end = al(off + 8ull * n);
+        copy = gapless ? off : end;
+    }
+};
+
+// The pipelined form of a large synchronous call (messages packed in order
+// in [0, total)).  The arena goes over PCIe in chunks on the xin stream
+// (straight from a page-locked caller arena, else packed by the host pool into
+// the pinned ring behind the previous chunks' DMA; the first chunk is small so
+// the DMA starts early); as soon as a chunk has landed, the request kernel
+// hashes every message that lies wholly inside the bytes received so far, and
+// the xout stream brings those digests back while the next chunks are still
+// coming in (PCIe is full duplex).  The lists kernel follows the last request
+// chunk.  A call then costs about its H2D time plus one chunk's kernel and
+// D2H, instead of H2D + kernels + D2H + host copy-out in sequence.
+// `gapless`: off[i] - shift = len[0] + ... + len[i-1].
+constexpr uint64_t kFirstChunk = 8ull << 20;
 int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const uint32_t* len, uint32_t n,
-                  uint64_t shift, const uint32_t* idx, const uint32_t* first, uint32_t n_lists, uint8_t* req_out,
-                  uint8_t* list_out) {
+                  uint64_t shift, bool gapless, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
+                  uint8_t* req_out, uint8_t* list_out) {
     double t_pack = 0.0, t_wait = 0.0, t_out = 0.0;
+    // MIRSHA_STAGE_TRACE=1: one line per call on stderr with the host time
+    // (us since entry) at which each chunk was queued and each wait returned.
+    const bool trace = getenv_flag("MIRSHA_STAGE_TRACE");
+    const auto t_entry = Clock::now();
+    std::string tl;
+    auto mark = [&](const char* what, uint32_t k) {
+        if (!trace) return;
+        char b[48];
+        snprintf(b, sizeof b, " %s%u@%.0f", what, k, ms_since(t_entry) * 1e3);
+        tl += b;
+    };
     const uint64_t total = src.total;
     const uint32_t entries = n_lists ? first[n_lists] : 0u;
-    const uint32_t nch = (uint32_t)((total + kStageChunk - 1) / kStageChunk);
+    // Chunk k covers arena bytes [cb[k], cb[k+1]).
+    std::vector<uint64_t> cb{0};
+    for (uint64_t x = std::min(total, kFirstChunk); ; x = std::min(total, x + kStageChunk)) {
+        cb.push_back(x);
+        if (x == total) break;
+    }
+    const uint32_t nch = (uint32_t)cb.size() - 1;
     if (!c->xin) HIP_TRY(c, hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
     if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
     // events: in[k], kern[k], out[k] per chunk; meta; lists kernel; lists out
@@ -466,7 +517,7 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     uint8_t* d_arena = c->d_arena.as<uint8_t>();
     const bool pinned_src = src.base && host_pinned(src.base);
     auto queue_in = [&](uint32_t k) -> int {
-        const uint64_t a = (uint64_t)k * kStageChunk, b = std::min(total, a + kStageChunk);
+        const uint64_t a = cb[k], b = cb[k + 1];
         const uint8_t* from = pinned_src ? src.base + a : nullptr;
         if (!from) {
             const int slot = (int)(k % kStageSlots);
@@ -483,16 +534,17 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         }
         HIP_TRY(c, hipMemcpyAsync(d_arena + a, from, b - a, hipMemcpyHostToDevice, c->xin));
         HIP_TRY(c, hipEventRecord(ev_in[k], c->xin));
+        mark("in", k);
         return MIRSHA_OK;
     };
     if (int rc = queue_in(0)) return rc;
 
     // Metadata (behind chunk 0 on the same copy stream).  Chunk k hashes the
-    // messages [cut[k], cut[k+1]): those ending within its first B_k bytes.
+    // messages [cut[k], cut[k+1]): those ending within its bytes [0, cb[k+1]).
     const auto tp = Clock::now();
     std::vector<uint32_t> cut(nch + 1, 0);
     for (uint32_t k = 0; k + 1 < nch; k++) {
-        const uint64_t bk = (uint64_t)(k + 1) * kStageChunk;
+        const uint64_t bk = cb[k + 1];
         uint32_t lo = cut[k], hi = n;  // first i with end(i) > bk (ends are nondecreasing)
         while (lo < hi) {
             const uint32_t mid = lo + (hi - lo) / 2;
@@ -501,11 +553,33 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         cut[k + 1] = lo;
     }
     cut[nch] = n;
-    MetaLayout L(n, true, entries, n_lists, 0);
-    HIP_TRY(c, c->h_meta.ensure(L.end));
-    HIP_TRY(c, c->d_meta.ensure(L.end));
+    // Lengths first (and whether the block counts differ), then the layout.
+    HIP_TRY(c, c->h_meta.ensure(PipeLayout(n, entries, n_lists, true, false).end));
     uint8_t* h = c->h_meta.as<uint8_t>();
-    const bool ordered = meta_fill(off, len, n, shift, h, L);
+    std::atomic<uint32_t> lo_b{UINT32_MAX}, hi_b{0};
+    mirsha::host::parallel_for(n, mirsha::host::threads_for(4ull * n, n), [&](uint32_t a, uint32_t b) {
+        uint32_t* hl = reinterpret_cast<uint32_t*>(h);
+        uint32_t lo = UINT32_MAX, hi = 0;
+        for (uint32_t i = a; i < b; i++) {
+            hl[i] = len[i];
+            const uint32_t k = host_blocks(len[i]);
+            lo = std::min(lo, k);
+            hi = std::max(hi, k);
+        }
+        uint32_t cur = lo_b.load();
+        while (lo < cur && !lo_b.compare_exchange_weak(cur, lo)) {}
+        cur = hi_b.load();
+        while (hi > cur && !hi_b.compare_exchange_weak(cur, hi)) {}
+    });
+    const bool ordered = lo_b.load() != hi_b.load();
+    const PipeLayout L(n, entries, n_lists, ordered, gapless);
+    HIP_TRY(c, c->d_meta.ensure(L.end));
+    if (!gapless) {
+        uint64_t* ho = reinterpret_cast<uint64_t*>(h + L.off);
+        mirsha::host::parallel_for(n, mirsha::host::threads_for(8ull * n, n), [&](uint32_t a, uint32_t b) {
+            for (uint32_t i = a; i < b; i++) ho[i] = off[i] - shift;
+        });
+    }
     if (ordered) {  // a bucket order per chunk, indices local to the chunk
         mirsha::host::parallel_for(nch, (int)nch, [&](uint32_t a, uint32_t b) {
             for (uint32_t k = a; k < b; k++)
@@ -514,11 +588,20 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     }
     if (entries) pmemcpy(h + L.idx, idx, 4ull * entries);
     if (n_lists) pmemcpy(h + L.first, first, 4ull * (n_lists + 1));
-    HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.end, hipMemcpyHostToDevice, c->xin));
+    HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.copy, hipMemcpyHostToDevice, c->xin));
     HIP_TRY(c, hipEventRecord(ev_meta, c->xin));
     HIP_TRY(c, hipStreamWaitEvent(c->stream, ev_meta, 0));
-    c->prof[MIRSHA_PROF_PLAN] = ms_since(tp);
     uint8_t* dm = c->d_meta.as<uint8_t>();
+    if (gapless) {  // off = exclusive scan of len, on the device
+        size_t tb = 0;
+        HIP_TRY(c, mirsha::launch_offsets_scan(nullptr, tb, reinterpret_cast<const uint32_t*>(dm + L.len),
+                                               reinterpret_cast<uint64_t*>(dm + L.off), n, c->stream));
+        HIP_TRY(c, c->d_scan.ensure(std::max<size_t>(tb, 4)));
+        HIP_TRY(c, mirsha::launch_offsets_scan(c->d_scan.p, tb, reinterpret_cast<const uint32_t*>(dm + L.len),
+                                               reinterpret_cast<uint64_t*>(dm + L.off), n, c->stream));
+    }
+    c->prof[MIRSHA_PROF_PLAN] = ms_since(tp);
+    mark("meta", 0);
 
     const uint64_t out_bytes = 32ull * ((uint64_t)n + n_lists);
     HIP_TRY(c, c->d_out.ensure(std::max<uint64_t>(out_bytes, 32)));
@@ -530,11 +613,12 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     uint8_t* h_lst = direct_out ? c->h_outs.as<uint8_t>() : h_req + 32ull * n;
 
     uint32_t copied = 0;  // chunks whose digests are in req_out
-    auto copy_out = [&](uint32_t k) {
-        if (!direct_out && cut[k + 1] > cut[k]) {
+    auto copy_out = [&](uint32_t k0, uint32_t k1) {  // chunks [k0, k1), one parallel copy
+        if (!direct_out && cut[k1] > cut[k0]) {
             const auto w = Clock::now();
-            pmemcpy(req_out + 32ull * cut[k], h_req + 32ull * cut[k], 32ull * (cut[k + 1] - cut[k]));
+            pmemcpy(req_out + 32ull * cut[k0], h_req + 32ull * cut[k0], 32ull * (cut[k1] - cut[k0]));
             t_out += ms_since(w);
+            mark("out", k1);
         }
     };
     for (uint32_t k = 0; k < nch; k++) {
@@ -556,7 +640,10 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         if (cnt) HIP_TRY(c, hipMemcpyAsync(h_req + 32ull * i0, d_req + 32ull * i0, 32ull * cnt, hipMemcpyDeviceToHost, c->xout));
         HIP_TRY(c, hipEventRecord(ev_out[k], c->xout));
         // digests that are already back go to the caller while later chunks pack
-        while (copied < k && hipEventQuery(ev_out[copied]) == hipSuccess) copy_out(copied++);
+        uint32_t ready = copied;
+        while (ready < k && hipEventQuery(ev_out[ready]) == hipSuccess) ready++;
+        copy_out(copied, ready);
+        copied = ready;
     }
     (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
     if (n_lists) {
@@ -572,11 +659,22 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         HIP_TRY(c, hipMemcpyAsync(h_lst, d_lst, 32ull * n_lists, hipMemcpyDeviceToHost, c->xout));
         HIP_TRY(c, hipEventRecord(ev_lo, c->xout));
     }
-    for (; copied < nch; copied++) {
+    // The rest: all but the last chunk are usually back by now (one copy for
+    // them), then the last chunk and the lists.
+    if (copied + 1 < nch) {
         const auto w = Clock::now();
-        HIP_TRY(c, hipEventSynchronize(ev_out[copied]));
+        HIP_TRY(c, hipEventSynchronize(ev_out[nch - 2]));
         t_wait += ms_since(w);
-        copy_out(copied);
+        mark("w", nch - 2);
+        copy_out(copied, nch - 1);
+        copied = nch - 1;
+    }
+    if (copied < nch) {
+        const auto w = Clock::now();
+        HIP_TRY(c, hipEventSynchronize(ev_out[nch - 1]));
+        t_wait += ms_since(w);
+        mark("w", nch - 1);
+        copy_out(copied, nch);
     }
     if (n_lists) {
         const auto w = Clock::now();
@@ -584,6 +682,8 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         t_wait += ms_since(w);
         memcpy(list_out, h_lst, 32ull * n_lists);
     }
+    mark("end", nch);
+    if (trace) fprintf(stderr, "mirsha stage trace: %u chunks%s\n", nch, tl.c_str());
     // The caller's stream also saw every kernel finish (ev_out waits on them).
     c->prof[MIRSHA_PROF_PACK] = t_pack;
     c->prof[MIRSHA_PROF_DEVICE] = t_wait;
@@ -594,13 +694,16 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
 // One synchronous call: n messages (offsets minus `shift` are positions in the
 // packed arena) and optionally n_lists digest lists over their digests.
 // req_out / list_out are the caller's host buffers (n x 32, n_lists x 32).
-// `inorder`: the messages lie in [0, total) back to back in index order (each
-// starts at or after the previous one's end), which the pipelined form needs.
+// `layout`: kInOrder = the messages lie in [0, total) in index order (each
+// starts at or after the previous one's end), which the pipelined form needs;
+// kGapless = in order with no gaps (off[i] - shift = len[0] + ... + len[i-1]).
+enum ArenaLayout { kAnyOrder = 0, kInOrder = 1, kGapless = 2 };
 int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const uint32_t* len, uint32_t n,
-               uint64_t shift, bool inorder, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
+               uint64_t shift, ArenaLayout layout, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
                uint8_t* req_out, uint8_t* list_out) {
-    if (n && inorder && src.total > kStageChunk && !getenv_flag("MIRSHA_NO_PIPELINED_CALLS"))
-        return run_pipelined(c, src, off, len, n, shift, idx, first, n_lists, req_out, list_out);
+    if (n && layout != kAnyOrder && src.total > kStageChunk && !getenv_flag("MIRSHA_NO_PIPELINED_CALLS"))
+        return run_pipelined(c, src, off, len, n, shift, layout == kGapless && !getenv_flag("MIRSHA_NO_OFFSET_SCAN"),
+                             idx, first, n_lists, req_out, list_out);
     // Host phases into c->prof (mirsha_ctx_host_profile): pack = queueing the
     // request bytes, plan = metadata block, device = queue -> sync, scatter =
     // digests to the caller.  (validate is filled by the caller.)
@@ -680,20 +783,20 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
 }
 
 // Validates messages of a caller arena: the dense span [lo, hi) they cover,
-// their total length, and whether they lie back to back in index order
-// (off[i] >= off[i-1] + len[i-1]).  One parallel pass.
+// their total length, and their layout (in index order: off[i] >= off[i-1] +
+// len[i-1]; gapless: equality).  One parallel pass.
 int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uint32_t* len, uint32_t n,
-               uint64_t* lo_out, uint64_t* hi_out, uint64_t* total_out = nullptr, bool* inorder_out = nullptr) {
+               uint64_t* lo_out, uint64_t* hi_out, uint64_t* total_out = nullptr, ArenaLayout* layout_out = nullptr) {
     // Threads over index ranges; the first bad message (lowest index) is reported.
     const int T = mirsha::host::threads_for(12ull * n, n);
     std::vector<uint64_t> los(T, UINT64_MAX), his(T, 0), tot(T, 0);
     std::vector<uint32_t> bad(T, UINT32_MAX);
-    std::vector<uint8_t> ord(T, 1);
+    std::vector<uint8_t> ord(T, 1), tight(T, 1);
     const uint32_t step = (n + T - 1) / std::max(T, 1);
     mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
         const int k = (int)(a / std::max<uint32_t>(step, 1));
         uint64_t lo = UINT64_MAX, hi = 0, t = 0;
-        bool in = true;
+        bool in = true, gl = true;
         for (uint32_t i = a; i < b; i++) {
             if (len[i] > MIRSHA_MAX_MESSAGE_BYTES || off[i] > arena_len || len[i] > arena_len - off[i]) {
                 bad[k] = i;
@@ -703,11 +806,13 @@ int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uin
             hi = std::max<uint64_t>(hi, off[i] + len[i]);
             t += len[i];
             if (i && off[i] < off[i - 1] + len[i - 1]) in = false;
+            if (i && off[i] != off[i - 1] + len[i - 1]) gl = false;
         }
         los[k] = lo;
         his[k] = hi;
         tot[k] = t;
         ord[k] = in;
+        tight[k] = gl;
     });
     const uint32_t i = *std::min_element(bad.begin(), bad.end());
     if (i != UINT32_MAX) {
@@ -721,7 +826,10 @@ int arena_span(mirsha_ctx* c, uint64_t arena_len, const uint64_t* off, const uin
     uint64_t t = 0;
     for (uint64_t x : tot) t += x;
     if (total_out) *total_out = t;
-    if (inorder_out) *inorder_out = std::all_of(ord.begin(), ord.end(), [](uint8_t x) { return x != 0; });
+    if (layout_out) {
+        auto all = [](const std::vector<uint8_t>& v) { return std::all_of(v.begin(), v.end(), [](uint8_t x) { return x != 0; }); };
+        *layout_out = !all(ord) ? kAnyOrder : (all(tight) && (!n || off[0] == *lo_out) ? kGapless : kInOrder);
+    }
     return MIRSHA_OK;
 }
 
@@ -733,14 +841,16 @@ int run_arena_call(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, cons
     const auto t0 = Clock::now();
     for (double& x : c->prof) x = 0.0;
     uint64_t lo = 0, hi = 0, total = 0;
-    bool inorder = false;
-    if (int rc = arena_span(c, arena_len, off, len, n, &lo, &hi, &total, &inorder)) return rc;
+    ArenaLayout layout = kAnyOrder;
+    if (int rc = arena_span(c, arena_len, off, len, n, &lo, &hi, &total, &layout)) return rc;
     c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
     ArenaSrc src;
     if (hi - lo <= 2 * total + 4096) {  // dense: ship the span, offsets rebased on lo
         src.base = arena + lo;
         src.total = hi - lo;
-        return run_staged(c, src, off, len, n, lo, inorder, idx, first, n_lists, req_out, list_out);
+        const int rc = run_staged(c, src, off, len, n, lo, layout, idx, first, n_lists, req_out, list_out);
+        c->prof[MIRSHA_PROF_TOTAL] = ms_since(t0);
+        return rc;
     }
     // sparse: one slice per message, packed back to back
     std::vector<uint64_t> roff(n);
@@ -762,7 +872,9 @@ int run_arena_call(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, cons
     src.poff = roff.data();
     src.n = n;
     src.total = total;
-    return run_staged(c, src, roff.data(), len, n, 0, true, idx, first, n_lists, req_out, list_out);
+    const int rc = run_staged(c, src, roff.data(), len, n, 0, kGapless, idx, first, n_lists, req_out, list_out);
+    c->prof[MIRSHA_PROF_TOTAL] = ms_since(t0);
+    return rc;
 }
 
 // ---- request -> batch-digest plan (sequential form) ------------------------
@@ -1257,6 +1369,7 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     }
     c->d_arena.release(); c->d_off.release(); c->d_len.release(); c->d_order.release();
     c->d_out.release(); c->d_idx.release(); c->d_first.release(); c->d_out2.release(); c->d_scratch.release();
+    c->d_scan.release();
     for (int k = 0; k < kStageSlots; k++) {
         c->h_ring[k].release();
         if (c->ring_ev[k]) (void)hipEventDestroy(c->ring_ev[k]);
@@ -1375,7 +1488,9 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
     src.poff = poff.data();
     src.n = n;
     src.total = p;
-    return run_staged(c, src, poff.data(), len.data(), n, 0, true, nullptr, nullptr, 0, out, nullptr);
+    const int rc = run_staged(c, src, poff.data(), len.data(), n, 0, kGapless, nullptr, nullptr, 0, out, nullptr);
+    c->prof[MIRSHA_PROF_TOTAL] = ms_since(t0);
+    return rc;
 }
 
 int mirsha_host_alloc(mirsha_ctx* c, uint64_t bytes, void** out) {
@@ -1491,7 +1606,7 @@ int mirsha_hash_requests_then_batches(mirsha_ctx* c, const uint8_t* arena, uint6
     if (n_req == 0 && n_batches == 0) return MIRSHA_OK;
     if (n_req == 0) {  // lists of null requests only (every entry is MIRSHA_NULL_INDEX)
         ArenaSrc none;
-        return run_staged(c, none, nullptr, nullptr, 0, 0, false, idx, first, n_batches, nullptr, batch_out);
+        return run_staged(c, none, nullptr, nullptr, 0, 0, kAnyOrder, idx, first, n_batches, nullptr, batch_out);
     }
     return run_arena_call(c, arena, arena_len, off, len, n_req, idx, first, n_batches, req_out, batch_out);
 }
@@ -1582,7 +1697,7 @@ int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digest
     ArenaSrc src;  // the digests themselves are the arena the lists index
     src.base = digests;
     src.total = 32ull * n_digests;
-    return run_staged(c, src, nullptr, nullptr, 0, 0, false, idx, first, n_lists, nullptr, out);
+    return run_staged(c, src, nullptr, nullptr, 0, 0, kAnyOrder, idx, first, n_lists, nullptr, out);
 }
 
 int mirsha_hash_batch_device(mirsha_ctx* c, const uint8_t* d_arena, uint64_t arena_len,

@@ -36,6 +36,10 @@ uint32_t pair_max_groups();
 // Arenas up to kMaxBufferArena bytes use one 32-bit buffer descriptor; larger
 // ones (any size) the 64-bit per-lane addressed loader.
 constexpr uint64_t kMaxBufferArena = 0xFFFFFF00ull;
+// off[i] = len[0] + ... + len[i-1] (exclusive scan; mirsha_scan.hip).  With
+// tmp == nullptr only sets tmp_bytes (the scratch size for n requests).
+hipError_t launch_offsets_scan(void* tmp, size_t& tmp_bytes, const uint32_t* len, uint64_t* off, uint32_t n,
+                               hipStream_t s);
 hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
                        const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
                        int variant, hipStream_t s);

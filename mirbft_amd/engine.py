@@ -356,7 +356,7 @@ class Engine:
         """Config-5 message bytes of requests [first, first + count) at d_arena + d_off[r]."""
         self._check(self._lib.mirsha_synth_mixed_device(self.ctx, seed, first, count, d_off, d_arena))
 
-    HOST_PHASES = ("validate", "plan", "pack", "device", "scatter")
+    HOST_PHASES = ("validate", "plan", "pack", "device", "scatter", "total")
 
     def host_profile(self) -> dict:
         """Host-side phases (ms) of the last slice submission (mirsha_ctx_host_profile)."""

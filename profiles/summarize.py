@@ -27,6 +27,19 @@ def main(d):
         if k:
             out["kernels"].setdefault(k, {})["avg_ns"] = float(r["AverageNs"])
             out["kernels"][k]["calls"] = int(r["Calls"])
+    # Per launch shape from the kernel trace: the bench's own launches (full
+    # config grid) apart from the pipelined host calls' chunk launches.
+    tr = os.path.join(d, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        by = collections.defaultdict(list)
+        for r in csv.DictReader(open(tr)):
+            k = short(r["Kernel_Name"])
+            if k:
+                by[(k, int(r["Grid_Size_X"]))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+        for (k, g), v in by.items():
+            v.sort()
+            out["kernels"].setdefault(k, {}).setdefault("by_grid", {})[str(g)] = {
+                "launches": len(v), "mean_us": sum(v) / len(v), "median_us": v[len(v) // 2]}
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mem"):
         f = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(f):

@@ -144,3 +144,18 @@ def test_host_profile_phases(engine):
     prof = engine.host_profile()
     assert set(prof) >= {"validate", "plan", "pack", "device", "scatter"}
     assert all(v >= 0 for v in prof.values())
+
+
+def test_gapless_shifted_arena_device_offsets(engine, monkeypatch):
+    """Gapless requests at a nonzero base: the pipelined path ships only the
+    lengths and rebuilds the offsets by a device scan; equal to shipping them
+    (MIRSHA_NO_OFFSET_SCAN=1) and to the oracle.  Mixed lengths, so the
+    per-chunk bucket order rides along."""
+    rng = np.random.default_rng(25)
+    lens = rng.integers(0, 9000, 20000).astype(np.uint32)
+    off = 4096 + np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
+    arena = rng.integers(0, 256, int(off[-1] + lens[-1]) + 100, dtype=np.uint8)
+    assert arena.size > 2 * CHUNK
+    a = _check(engine, arena, off, lens)
+    monkeypatch.setenv("MIRSHA_NO_OFFSET_SCAN", "1")
+    assert np.array_equal(engine.hash_batch(arena, off, lens), a)

@@ -18,7 +18,7 @@ build() {
     local name=$1; shift
     mkdir -p tools/scratch/$name
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Itools "$@" -shared \
-        -o tools/scratch/$name/libmirsha.so $SRC/mirsha_kernels.hip $SRC/mirsha_api.hip $SRC/mirsha_host.cpp
+        -o tools/scratch/$name/libmirsha.so $SRC/mirsha_kernels.hip $SRC/mirsha_api.hip $SRC/mirsha_scan.hip $SRC/mirsha_host.cpp
 }
 build r1form -DMIRSHA_AB_KSGPR -DMIRSHA_AB_NOALIGNED -DMIRSHA_AB_OLDPROLOGUE &
 build oldpro -DMIRSHA_AB_OLDPROLOGUE &
