@@ -387,7 +387,8 @@ class MixedWorkload:
         eng.synth_mixed_lengths_device(self.seed, 0, g, d_all.data_ptr())
         eng.sync()
         lo, hi = sharding.shard_ranges(g, world, 1, d_all.cpu().numpy().view(np.uint32))[rank]
-        self.first_req, self.n = lo, n = hi - lo
+        n = hi - lo
+        self.first_req, self.n = lo, n
         self.global_requests = g
         d_len = d_all[lo:hi].clone()
         del d_all

@@ -694,6 +694,25 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
 // One synchronous call: n messages (offsets minus `shift` are positions in the
 // packed arena) and optionally n_lists digest lists over their digests.
 // req_out / list_out are the caller's host buffers (n x 32, n_lists x 32).
+// Largest block count of n messages (one parallel pass).
+uint32_t max_blocks(const uint32_t* len, uint32_t n) {
+    std::atomic<uint32_t> hi{0};
+    mirsha::host::parallel_for(n, mirsha::host::threads_for(4ull * n, n), [&](uint32_t a, uint32_t b) {
+        uint32_t m = 0;
+        for (uint32_t i = a; i < b; i++) m = std::max(m, len[i]);
+        uint32_t cur = hi.load();
+        while (m > cur && !hi.compare_exchange_weak(cur, m)) {}
+    });
+    return host_blocks(hi.load());
+}
+
+// Each chunk of a pipelined call is its own launch, and a launch takes at
+// least its longest message's chain (~2-2.5 us per block at one wave per
+// SIMD).  Past 256 blocks (16 KiB) that floor exceeds a 32 MiB chunk's DMA
+// (~0.55 ms) and chunked launches would serialise: 9 x 1.86 ms for config 4's
+// 61.6 KB acks (profiles/r02p) instead of one 1.86 ms launch.
+constexpr uint32_t kPipeMaxBlocks = 256;
+
 // `layout`: kInOrder = the messages lie in [0, total) in index order (each
 // starts at or after the previous one's end), which the pipelined form needs;
 // kGapless = in order with no gaps (off[i] - shift = len[0] + ... + len[i-1]).
@@ -701,7 +720,8 @@ enum ArenaLayout { kAnyOrder = 0, kInOrder = 1, kGapless = 2 };
 int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const uint32_t* len, uint32_t n,
                uint64_t shift, ArenaLayout layout, const uint32_t* idx, const uint32_t* first, uint32_t n_lists,
                uint8_t* req_out, uint8_t* list_out) {
-    if (n && layout != kAnyOrder && src.total > kStageChunk && !getenv_flag("MIRSHA_NO_PIPELINED_CALLS"))
+    if (n && layout != kAnyOrder && src.total > kStageChunk && !getenv_flag("MIRSHA_NO_PIPELINED_CALLS") &&
+        max_blocks(len, n) <= kPipeMaxBlocks)
         return run_pipelined(c, src, off, len, n, shift, layout == kGapless && !getenv_flag("MIRSHA_NO_OFFSET_SCAN"),
                              idx, first, n_lists, req_out, list_out);
     // Host phases into c->prof (mirsha_ctx_host_profile): pack = queueing the

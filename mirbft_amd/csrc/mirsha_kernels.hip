@@ -230,6 +230,30 @@ __device__ unsigned long long g_stamps[kStampWords * kStampTiles];
     } while (0)
 #endif
 
+// Issue priority of a request wave, set before each block's rounds: block b
+// runs at max(0, kPrioTop - b), so a wave that is behind wins issue over one
+// that is ahead.  The SIMD's arbiter otherwise runs its waves in age order:
+// the oldest finish first and the second generation inherits their spread,
+// which left the last ~80 us of a config-2 launch draining from 8 to 0 waves
+// per SIMD (profiles/r02n stamps).  Same-box A/B over two boxes
+// (profiles/r02p, profiles/r02r), config 2 request kernel: top 3 189.9 /
+// 190.1 us vs 193.8 / 193.3 us with every block at priority 0; tops 1 and 2
+// and a high top for the launch's last generation only were in between or
+// box-dependent.
+#ifndef MIRSHA_PRIO_TOP  // A/B builds override (tools/ab_build.sh)
+#define MIRSHA_PRIO_TOP 3
+#endif
+constexpr uint32_t kPrioTop = MIRSHA_PRIO_TOP;
+__device__ __forceinline__ void progress_prio(uint32_t blk) {
+#ifndef MIRSHA_AB_NOPRIO
+    const uint32_t p = blk < kPrioTop ? kPrioTop - blk : 0u;
+    if (p >= 3u) __builtin_amdgcn_s_setprio(3);
+    else if (p == 2u) __builtin_amdgcn_s_setprio(2);
+    else if (p == 1u) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+#endif
+}
+
 // One wave hashes the tile of 64 messages at processing positions
 // [64 t, 64 t + 64) (order[] maps a position to a message; NULL = identity).
 // kLds: LDS-staged coalesced loader (else direct per-lane loads); kWide:
@@ -414,9 +438,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                 asm volatile("s_sub_u32 %0, %1, %2" : "=s"(left) : "s"(wave_nb), "s"(blk));
                 pad_block_uniform(w, soff, min_l, left == 1u);
             }
-#ifndef MIRSHA_AB_NOPRIO
-            if (blk == 0u) __builtin_amdgcn_s_setprio(0);
-#endif
+            progress_prio(blk);
             if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm(st, w);
         }
@@ -457,9 +479,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifndef MIRSHA_AB_NOPRIO
-            if (blk == 0u) __builtin_amdgcn_s_setprio(0);
-#endif
+            progress_prio(blk);
             if (blk < nb) compress_asm(st, w);
         }
     } else {
@@ -472,9 +492,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
-#ifndef MIRSHA_AB_NOPRIO
-            if (blk == 0u) __builtin_amdgcn_s_setprio(0);
-#endif
+            progress_prio(blk);
             if (active) compress_asm(st, w);
         }
     }

@@ -11,6 +11,8 @@
 #   ppad:      -DMIRSHA_AB_PRODUCER_PAD (loader-side padding for uniform-length tiles too)
 #   occ6:      -DMIRSHA_AB_OCC6         (request kernel held to 6 waves/SIMD by LDS)
 #   pf5:       -DMIRSHA_AB_PREFETCH     (next block chunks prefetched into registers, 5 waves/SIMD)
+#   spawn:     -DMIRSHA_AB_SPAWN_THREADS (host passes on threads spawned per call instead of the pool)
+#   prioN:     -DMIRSHA_PRIO_TOP=N      (block b's rounds at issue priority max(0, N - b); product 3)
 set -euo pipefail
 cd "$(dirname "$0")/.."
 SRC=mirbft_amd/csrc
@@ -28,5 +30,7 @@ build stamps -DMIRSHA_AB_STAMPS &
 build ppad -DMIRSHA_AB_PRODUCER_PAD &
 build occ6 -DMIRSHA_AB_OCC6 &
 build pf5 -DMIRSHA_AB_PREFETCH &
+build spawn -DMIRSHA_AB_SPAWN_THREADS &
+build prio0 -DMIRSHA_PRIO_TOP=0 &
 wait
 ls -la tools/scratch/*/libmirsha.so
