@@ -244,15 +244,9 @@ __device__ unsigned long long g_stamps[kStampWords * kStampTiles];
 #define MIRSHA_PRIO_TOP 3
 #endif
 constexpr uint32_t kPrioTop = MIRSHA_PRIO_TOP;
-__device__ __forceinline__ void progress_prio(uint32_t blk, uint32_t wave_nb) {
+__device__ __forceinline__ void progress_prio(uint32_t blk) {
 #ifndef MIRSHA_AB_NOPRIO
-#ifdef MIRSHA_AB_PRIO_FRAC  // A/B build only: priority by the fraction of the tile done
-    const uint32_t q = (4u * blk) / (wave_nb ? wave_nb : 1u);
-    const uint32_t p = q < 3u ? 3u - q : 0u;
-#else
-    (void)wave_nb;
     const uint32_t p = blk < kPrioTop ? kPrioTop - blk : 0u;
-#endif
     if (p >= 3u) __builtin_amdgcn_s_setprio(3);
     else if (p == 2u) __builtin_amdgcn_s_setprio(2);
     else if (p == 1u) __builtin_amdgcn_s_setprio(1);
@@ -444,7 +438,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                 asm volatile("s_sub_u32 %0, %1, %2" : "=s"(left) : "s"(wave_nb), "s"(blk));
                 pad_block_uniform(w, soff, min_l, left == 1u);
             }
-            progress_prio(blk, wave_nb);
+            progress_prio(blk);
             if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm(st, w);
         }
@@ -485,7 +479,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            progress_prio(blk, wave_nb);
+            progress_prio(blk);
             if (blk < nb) compress_asm(st, w);
         }
     } else {
@@ -498,7 +492,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 finish_chunk(rc[q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
-            progress_prio(blk, wave_nb);
+            progress_prio(blk);
             if (active) compress_asm(st, w);
         }
     }

@@ -13,7 +13,6 @@
 #   pf5:       -DMIRSHA_AB_PREFETCH     (next block chunks prefetched into registers, 5 waves/SIMD)
 #   spawn:     -DMIRSHA_AB_SPAWN_THREADS (host passes on threads spawned per call instead of the pool)
 #   prioN:     -DMIRSHA_PRIO_TOP=N      (block b's rounds at issue priority max(0, N - b), clamped to 3; product 3)
-#   priofrac:  -DMIRSHA_AB_PRIO_FRAC    (priority 3 - quarter of the tile's blocks done)
 set -euo pipefail
 cd "$(dirname "$0")/.."
 SRC=mirbft_amd/csrc
@@ -34,7 +33,5 @@ build pf5 -DMIRSHA_AB_PREFETCH &
 build spawn -DMIRSHA_AB_SPAWN_THREADS &
 build prio0 -DMIRSHA_PRIO_TOP=0 &
 build prio4 -DMIRSHA_PRIO_TOP=4 &
-build prio5 -DMIRSHA_PRIO_TOP=5 &
-build priofrac -DMIRSHA_AB_PRIO_FRAC &
 wait
 ls -la tools/scratch/*/libmirsha.so
