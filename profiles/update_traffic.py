@@ -35,7 +35,7 @@ def main():
         "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],
         "FETCH_SIZE_kb": k.get("FETCH_SIZE"), "WRITE_SIZE_kb": k.get("WRITE_SIZE"),
         "TCC_HIT_sum": k.get("TCC_HIT_sum"), "TCC_MISS_sum": k.get("TCC_MISS_sum"),
-        "source": f"profiles/{a.tag}/summary.json (profiles/profile.sh {a.tag})",
+        "source": f"{a.summary} (profiles/profile.sh {a.tag})",
     }
     if a.algorithmic:
         entry["over_algorithmic"] = k["hbm_bytes_per_launch"] / a.algorithmic
