@@ -643,15 +643,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal knobs for the N>1 path on a one-GPU box (never set by the
+    # driver): every rank on device MIRSHA_BENCH_DEVICE, barriers and
+    # reductions over gloo instead of RCCL.
+    if os.environ.get("MIRSHA_BENCH_DEVICE"):
+        local = int(os.environ["MIRSHA_BENCH_DEVICE"])
+    backend = os.environ.get("MIRSHA_BENCH_DIST_BACKEND", "nccl")
     dist = None
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    # reductions live on the device for RCCL, on the host for gloo
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     eng = Engine(local)
     eng.set_variant(a.variant)
@@ -725,7 +734,7 @@ def main():
         probe = {"clock_ghz": ghz, "cycles_per_wave_compression": cyc}
 
     if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -734,7 +743,7 @@ def main():
 
     # Whole-job totals: the sum over ranks (config 5's block-balanced shards
     # differ in request count per rank).
-    tot = torch.tensor([float(wl.digests), float(wl.bytes_hashed)], dtype=torch.float64, device=dev)
+    tot = torch.tensor([float(wl.digests), float(wl.bytes_hashed)], dtype=torch.float64, device=red_dev)
     if dist:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     value = float(tot[0].item()) * a.steps / dt

@@ -39,19 +39,28 @@ bool weak_fp() {
 
 inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 
-// Streaming word hash with a byte carry, so slicing does not matter.
+// Streaming word hash with a byte carry, so slicing does not matter: word k
+// of the concatenated stream (8 bytes, little-endian) feeds lane k & 3, each
+// lane one xor-multiply-rotate step (four independent chains, ~1.3 cycles per
+// word).  Equal fingerprints are only candidates: dedup confirms every match
+// byte for byte, so the hash needs spread, not collision resistance.
 struct Fp {
-    uint64_t h0 = 0x6D69726274667030ull, h1 = 0x9E3779B97F4A7C15ull;
+    uint64_t h[4] = {0x6D69726274667030ull, 0x9E3779B97F4A7C15ull, 0xC2B2AE3D27D4EB4Full, 0x165667B19E3779F9ull};
     uint64_t carry = 0, total = 0;
     int nc = 0;
-    uint64_t parity = 0;
-    inline void word(uint64_t w) {
-        // two interleaved lanes (word parity) keep the multiply chains short
-        if (parity++ & 1) {
-            h1 = rotl(h1 ^ (w * 0xBF58476D1CE4E5B9ull), 29) * 0x94D049BB133111EBull;
-        } else {
-            h0 = rotl(h0 ^ (w * 0x94D049BB133111EBull), 31) * 0xBF58476D1CE4E5B9ull;
-        }
+    uint64_t idx = 0;  // words consumed
+    static constexpr uint64_t kM[4] = {0x94D049BB133111EBull, 0xBF58476D1CE4E5B9ull, 0xD6E8FEB86659FD93ull,
+                                       0x9FB21C651E98DF25ull};
+    inline void lane(int k, uint64_t w) { h[k] = rotl((h[k] ^ w) * kM[k], 23 + 8 * k); }
+    inline void word(uint64_t w) { lane((int)(idx++ & 3u), w); }
+    inline void words4(const uint8_t* p) {  // 4 words from a 4-aligned word index
+        uint64_t a[4];
+        memcpy(a, p, 32);
+        lane(0, a[0]);
+        lane(1, a[1]);
+        lane(2, a[2]);
+        lane(3, a[3]);
+        idx += 4;
     }
     void bytes(const uint8_t* p, uint64_t n) {
         total += n;
@@ -60,23 +69,14 @@ struct Fp {
             n--;
             if (++nc == 8) { word(carry); carry = 0; nc = 0; }
         }
-        if ((parity & 1) && n >= 8) {  // realign so word k always feeds lane k & 1
+        while ((idx & 3u) && n >= 8) {  // realign so word k always feeds lane k & 3
             uint64_t a;
             memcpy(&a, p, 8);
             word(a);
             p += 8;
             n -= 8;
         }
-        while (n >= 16) {  // = word(a); word(b) from an even parity
-            uint64_t a, b;
-            memcpy(&a, p, 8);
-            memcpy(&b, p + 8, 8);
-            h0 = rotl(h0 ^ (a * 0x94D049BB133111EBull), 31) * 0xBF58476D1CE4E5B9ull;
-            h1 = rotl(h1 ^ (b * 0xBF58476D1CE4E5B9ull), 29) * 0x94D049BB133111EBull;
-            parity += 2;
-            p += 16;
-            n -= 16;
-        }
+        for (; n >= 32; p += 32, n -= 32) words4(p);
         while (n >= 8) {
             uint64_t a;
             memcpy(&a, p, 8);
@@ -92,11 +92,11 @@ struct Fp {
     }
     uint64_t final() {
         if (nc) word(carry ^ ((uint64_t)nc << 56));
-        uint64_t h = h0 ^ rotl(h1, 17) ^ total * 0xD6E8FEB86659FD93ull;
-        h ^= h >> 32;
-        h *= 0xD6E8FEB86659FD93ull;
-        h ^= h >> 29;
-        return h;
+        uint64_t x = h[0] ^ rotl(h[1], 17) ^ rotl(h[2], 31) ^ rotl(h[3], 47) ^ total * 0xD6E8FEB86659FD93ull;
+        x ^= x >> 32;
+        x *= 0xD6E8FEB86659FD93ull;
+        x ^= x >> 29;
+        return x;
     }
 };
 
@@ -219,13 +219,60 @@ void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, ui
 uint64_t fingerprint(const uint8_t* const* ptr, const uint64_t* len, uint32_t s0, uint32_t s1) {
     if (weak_fp()) return 0;
     Fp f;
-    for (uint32_t s = s0; s < s1; s++)
-        if (len[s]) f.bytes(ptr[s], len[s]);
+    for (uint32_t s = s0; s < s1; s++) {
+        const uint64_t L = len[s];
+        const uint8_t* p = ptr[s];
+        if (f.nc == 0 && L == 8) {
+            // Whole words at a word boundary of the stream (every slice of
+            // epochChangeHashData: 8-byte LE64 fields and 32-byte digests,
+            // stateless.go:311-340): no carry to thread through.
+            uint64_t w;
+            memcpy(&w, p, 8);
+            f.total += 8;
+            f.word(w);
+        } else if (f.nc == 0 && L == 32 && (f.idx & 3u) == 0) {
+            f.total += 32;
+            f.words4(p);
+        } else if (L) {
+            f.bytes(p, L);
+        }
+    }
     return f.final();
 }
 
+namespace {
+inline bool eq_bytes(const uint8_t* p, const uint8_t* q, uint64_t n) {
+    if (p == q) return true;
+    if (n == 8) {
+        uint64_t x, y;
+        memcpy(&x, p, 8);
+        memcpy(&y, q, 8);
+        return x == y;
+    }
+    if (n == 32) {
+        uint64_t x[4], y[4];
+        memcpy(x, p, 32);
+        memcpy(y, q, 32);
+        return ((x[0] ^ y[0]) | (x[1] ^ y[1]) | (x[2] ^ y[2]) | (x[3] ^ y[3])) == 0;
+    }
+    return memcmp(p, q, n) == 0;
+}
+}  // namespace
+
 bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, uint32_t a1, uint32_t b0,
                   uint32_t b1) {
+    // Same slicing (the usual case: two copies of one message type): compare
+    // slice by slice; any difference in the slice lengths falls through to
+    // the general walk over the concatenations.
+    if (a1 - a0 == b1 - b0) {
+        uint32_t k = 0;
+        for (; k < a1 - a0; k++) {
+            const uint64_t L = len[a0 + k];
+            if (L != len[b0 + k]) break;
+            if (!eq_bytes(ptr[a0 + k], ptr[b0 + k], L)) return false;
+        }
+        if (k == a1 - a0) return true;
+    }
     uint32_t sa = a0, sb = b0;
     uint64_t pa = 0, pb = 0;  // positions inside the current slices
     for (;;) {
