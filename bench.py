@@ -249,7 +249,14 @@ class BatchWorkload:
         k = 256
         arena = o.gen_requests(self.seed, self.first_req, k, self.data_len)
         want = o.hash_requests(arena, np.arange(k, dtype=np.uint64) * self.stride, np.full(k, self.stride))
-        return bool(np.array_equal(self.d_req[:k].cpu().numpy(), want))
+        ok = bool(np.array_equal(self.d_req[:k].cpu().numpy(), want))
+        # and the first batch digests over those requests
+        nb = int(np.searchsorted(self.first, k, side="right")) - 1
+        if nb > 0:
+            torch.cuda.synchronize(self.d_req.device)
+            wb = o.batch_digests(want, self.idx[: self.first[nb]], self.first[: nb + 1])
+            ok = ok and bool(np.array_equal(self.d_bat[:nb].cpu().numpy(), wb))
+        return ok
 
     def pcie(self):
         n, stride = self.n, self.stride
