@@ -1266,69 +1266,101 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
     if (sl.busy)
         if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
-    // Plan: which requests reach the GPU (all, or one per distinct content).
-    std::vector<uint32_t> which;  // unique request indices, ascending (empty = all)
+    // Which requests reach the GPU: all, or one per distinct content.  With
+    // dedup the fingerprint heads (every one of them a final representative)
+    // are packed and queued first; the byte-for-byte confirmation of the
+    // duplicates then runs on the host while the GPU hashes the heads, and
+    // representatives found only there (fingerprint collisions, rare) follow
+    // in a second launch.
+    const bool dedup = (flags & MIRSHA_SUBMIT_DEDUP) && n > 1;
+    std::vector<uint32_t> which;  // requests in digest-row order (empty = all, identity)
+    std::vector<uint64_t> fp;
+    std::vector<uint32_t> tent;
+    std::vector<uint64_t> rl;
     sl.rank.clear();
-    uint32_t m = n;
-    if ((flags & MIRSHA_SUBMIT_DEDUP) && n > 1) {
-        std::vector<uint64_t> rl(len.begin(), len.end());
-        std::vector<uint32_t> rep(n);
-        m = mirsha::host::dedup_plan(slice_ptr, slice_len, slice_first, n, rl.data(), rep.data());
-        if (m < n) {
-            which.reserve(m);
-            sl.rank.resize(n);
-            for (uint32_t i = 0; i < n; i++) {
-                if (rep[i] == i) {
-                    sl.rank[i] = (uint32_t)which.size();
-                    which.push_back(i);
-                } else {
-                    sl.rank[i] = sl.rank[rep[i]];
-                }
-            }
-        }
+    if (dedup) {
+        rl.assign(len.begin(), len.end());
+        fp.resize(n);
+        tent.resize(n);
+        const uint32_t heads = mirsha::host::dedup_candidates(slice_ptr, slice_len, slice_first, n, rl.data(),
+                                                              fp.data(), tent.data());
+        which.reserve(heads);
+        for (uint32_t i = 0; i < n; i++)
+            if (tent[i] == i) which.push_back(i);
     }
-    if (n_unique_out) *n_unique_out = m;
     c->prof[MIRSHA_PROF_PLAN] = ms_since(t0);
     t0 = Clock::now();
-    std::vector<uint64_t> poff(m);
-    std::vector<uint32_t> plen(m);
-    uint64_t bytes = 0;
-    for (uint32_t k = 0; k < m; k++) {
-        const uint32_t i = which.empty() ? k : which[k];
-        poff[k] = bytes;
-        plen[k] = len[i];
-        bytes += len[i];
-    }
-    if (bytes + kArenaSlack > MIRSHA_MAX_DEVICE_ARENA_BYTES)
-        return fail(c, MIRSHA_ERANGE, "submission of %llu bytes exceeds one device arena (%u); split it",
-                    (unsigned long long)bytes, MIRSHA_MAX_DEVICE_ARENA_BYTES);
-    const uint64_t o_off = align8(bytes + kArenaSlack);
-    const uint64_t o_len = o_off + 8ull * m, o_ord = o_len + 4ull * m, o_end = align8(o_ord + 4ull * m);
-    const uint64_t o_dig = o_end;
-    HIP_TRY(c, sl.stage.ensure(o_end));
-    HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(m, 1)));
-    HIP_TRY(c, sl.dev.ensure(o_dig + 32ull * std::max<uint32_t>(m, 1)));
+    HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
     if (!sl.done) HIP_TRY(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-    uint8_t* st = sl.stage.as<uint8_t>();
-    mirsha::host::pack(slice_ptr, slice_len, slice_first, which.empty() ? nullptr : which.data(), m, poff.data(), st,
-                       mirsha::host::threads_for(bytes, m));
-    memcpy(st + o_off, poff.data(), 8ull * m);
-    memcpy(st + o_len, plen.data(), 4ull * m);
-    const bool identity = bucket_order(plen.data(), m, reinterpret_cast<uint32_t*>(st + o_ord));
+    // Packs requests `ids` (identity when null) and queues their digests into
+    // rows [row0, row0 + m) of sl.dig.
+    auto queue = [&](const uint32_t* ids, uint32_t m, uint32_t row0) -> int {
+        std::vector<uint64_t> poff(m);
+        std::vector<uint32_t> plen(m);
+        uint64_t bytes = 0;
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t i = ids ? ids[k] : k;
+            poff[k] = bytes;
+            plen[k] = len[i];
+            bytes += len[i];
+        }
+        if (bytes + kArenaSlack > MIRSHA_MAX_DEVICE_ARENA_BYTES)
+            return fail(c, MIRSHA_ERANGE, "submission of %llu bytes exceeds one device arena (%u); split it",
+                        (unsigned long long)bytes, MIRSHA_MAX_DEVICE_ARENA_BYTES);
+        const uint64_t o_off = align8(bytes + kArenaSlack);
+        const uint64_t o_len = o_off + 8ull * m, o_ord = o_len + 4ull * m, o_end = align8(o_ord + 4ull * m);
+        const uint64_t o_dig = o_end;
+        HIP_TRY(c, sl.stage.ensure(o_end));
+        HIP_TRY(c, sl.dev.ensure(o_dig + 32ull * std::max<uint32_t>(m, 1)));
+        uint8_t* st = sl.stage.as<uint8_t>();
+        mirsha::host::pack(slice_ptr, slice_len, slice_first, ids, m, poff.data(), st,
+                           mirsha::host::threads_for(bytes, m));
+        memcpy(st + o_off, poff.data(), 8ull * m);
+        memcpy(st + o_len, plen.data(), 4ull * m);
+        const bool identity = bucket_order(plen.data(), m, reinterpret_cast<uint32_t*>(st + o_ord));
+        uint8_t* dv = sl.dev.as<uint8_t>();
+        if (m) {
+            HIP_TRY(c, hipMemcpyAsync(dv, st, o_end, hipMemcpyHostToDevice, c->stream));
+            int rc = timed_launch(c, 0, [&] {
+                return mirsha::launch_msgs(dv, bytes, reinterpret_cast<const uint64_t*>(dv + o_off),
+                                           reinterpret_cast<const uint32_t*>(dv + o_len),
+                                           identity ? nullptr : reinterpret_cast<const uint32_t*>(dv + o_ord), m,
+                                           dv + o_dig, c->variant, c->stream);
+            });
+            if (rc) return rc;
+            HIP_TRY(c, hipMemcpyAsync(sl.dig.as<uint8_t>() + 32ull * row0, dv + o_dig, 32ull * m,
+                                      hipMemcpyDeviceToHost, c->stream));
+        }
+        return MIRSHA_OK;
+    };
+    uint32_t m = dedup ? (uint32_t)which.size() : n;
+    if (int rc = queue(dedup ? which.data() : nullptr, m, 0)) return rc;
     c->prof[MIRSHA_PROF_PACK] = ms_since(t0);
     sl.t_queued = Clock::now();
-    uint8_t* dv = sl.dev.as<uint8_t>();
-    if (m) {
-        HIP_TRY(c, hipMemcpyAsync(dv, st, o_end, hipMemcpyHostToDevice, c->stream));
-        int rc = timed_launch(c, 0, [&] {
-            return mirsha::launch_msgs(dv, bytes, reinterpret_cast<const uint64_t*>(dv + o_off),
-                                       reinterpret_cast<const uint32_t*>(dv + o_len),
-                                       identity ? nullptr : reinterpret_cast<const uint32_t*>(dv + o_ord), m,
-                                       dv + o_dig, c->variant, c->stream);
-        });
-        if (rc) return rc;
-        HIP_TRY(c, hipMemcpyAsync(sl.dig.p, dv + o_dig, 32ull * m, hipMemcpyDeviceToHost, c->stream));
+    if (dedup) {
+        t0 = Clock::now();
+        std::vector<uint32_t> rep(n);
+        const uint32_t distinct = mirsha::host::dedup_resolve(slice_ptr, slice_len, slice_first, n, rl.data(),
+                                                              fp.data(), tent.data(), rep.data());
+        sl.rank.resize(n);
+        for (uint32_t k = 0; k < m; k++) sl.rank[which[k]] = k;
+        const bool heads_only = distinct == m;
+        if (distinct > m) {  // collided requests that are representatives of their own
+            std::vector<uint32_t> extra;
+            for (uint32_t i = 0; i < n; i++)
+                if (rep[i] == i && tent[i] != i) {
+                    sl.rank[i] = m + (uint32_t)extra.size();
+                    extra.push_back(i);
+                }
+            HIP_TRY(c, hipStreamSynchronize(c->stream));  // the first launch's staging buffers are reused
+            if (int rc = queue(extra.data(), (uint32_t)extra.size(), m)) return rc;
+            m += (uint32_t)extra.size();
+        }
+        for (uint32_t i = 0; i < n; i++) sl.rank[i] = sl.rank[rep[i]];
+        if (heads_only && m == n) sl.rank.clear();  // all distinct: rows are already in origin order
+        c->prof[MIRSHA_PROF_PLAN] += ms_since(t0);
     }
+    if (n_unique_out) *n_unique_out = m;
     HIP_TRY(c, hipEventRecord(sl.done, c->stream));
     sl.busy = true;
     sl.user_out = out;

@@ -287,28 +287,35 @@ bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, u
     }
 }
 
-uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                    const uint64_t* req_len, uint32_t* rep) {
+uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                          const uint64_t* req_len, uint64_t* fp, uint32_t* tent) {
     if (n == 0) return 0;
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; i++) total += req_len[i];
-    const int threads = threads_for(total, n);
-    std::vector<uint64_t> fp(n);
-    parallel_for(n, threads, [&](uint32_t lo, uint32_t hi) {
+    parallel_for(n, threads_for(total, n), [&](uint32_t lo, uint32_t hi) {
         for (uint32_t i = lo; i < hi; i++) fp[i] = fingerprint(ptr, len, first[i], first[i + 1]);
     });
     // Tentative representative: first request with the same (fingerprint, length).
     std::unordered_map<uint64_t, uint32_t> head;
     head.reserve((size_t)n * 2);
-    std::vector<uint32_t> tent(n);
+    uint32_t heads = 0;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t key = fp[i] ^ (req_len[i] * 0x9E3779B97F4A7C15ull);
         auto it = head.emplace(key, i).first;
         tent[i] = it->second;
+        heads += tent[i] == i;
     }
+    return heads;
+}
+
+uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                       const uint64_t* req_len, const uint64_t* fp, const uint32_t* tent, uint32_t* rep) {
+    if (n == 0) return 0;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += req_len[i];
     // Confirm byte for byte (in parallel); a mismatch is a fingerprint collision.
     std::vector<uint8_t> ok(n, 1);
-    parallel_for(n, threads, [&](uint32_t lo, uint32_t hi) {
+    parallel_for(n, threads_for(total, n), [&](uint32_t lo, uint32_t hi) {
         for (uint32_t i = lo; i < hi; i++) {
             const uint32_t j = tent[i];
             if (j != i)
@@ -351,6 +358,15 @@ uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32
     // request equal to tent[i] (the key's first index) has rep tent[i]; the
     // first member of any other class under the key entered `reps` above.
     return distinct;
+}
+
+uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                    const uint64_t* req_len, uint32_t* rep) {
+    if (n == 0) return 0;
+    std::vector<uint64_t> fp(n);
+    std::vector<uint32_t> tent(n);
+    dedup_candidates(ptr, len, first, n, req_len, fp.data(), tent.data());
+    return dedup_resolve(ptr, len, first, n, req_len, fp.data(), tent.data(), rep);
 }
 
 void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,

@@ -36,9 +36,21 @@ bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, u
 
 // rep[i] = the smallest j <= i whose request bytes equal request i's (i if
 // none).  req_len[i] = total bytes of request i.  Returns the number of
-// distinct requests (rep[i] == i).
+// distinct requests (rep[i] == i).  = dedup_candidates + dedup_resolve.
 uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
                     const uint64_t* req_len, uint32_t* rep);
+
+// First half of dedup_plan: fingerprints fp[i] and tentative representatives
+// tent[i] = the first request with the same (fingerprint, length).  Returns
+// the number of heads (tent[i] == i); every head is a final representative,
+// so their hashing may start before dedup_resolve confirms the rest.
+uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                          const uint64_t* req_len, uint64_t* fp, uint32_t* tent);
+
+// Second half: confirms every tentative match byte for byte and resolves
+// fingerprint collisions; fills rep[] as dedup_plan.  Returns distinct count.
+uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                       const uint64_t* req_len, const uint64_t* fp, const uint32_t* tent, uint32_t* rep);
 
 // Copies request which[k] (k < m) to dst + dst_off[k], in parallel.
 void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,

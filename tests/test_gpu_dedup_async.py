@@ -197,3 +197,36 @@ def test_dropped_ticket_then_four_more(engine):
     for t, r in zip(ts, reqs[1:5]):
         assert rows(engine.wait(t)) == want(r)
     assert not engine._outstanding
+
+
+def test_dedup_collision_path_second_launch():
+    """MIRSHA_DEDUP_WEAK_FP=1 (read once per process, hence a subprocess):
+    every fingerprint is equal, so the heads queued before the byte-for-byte
+    confirmation are only one request per length, and every other distinct
+    request is found by the confirmation and hashed in the second launch.
+    Digests in origin order, dedup count exact, sync and async forms."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, hashlib; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "import torch; torch.cuda.is_available()\n"
+        "import test_host_dedup as t\n"
+        "from mirbft_amd import Engine\n"
+        "e = Engine(0)\n"
+        "for seed in (0, 1, 2):\n"
+        "    reqs = t.random_requests(seed, n=300)\n"
+        "    want = [hashlib.sha256(b''.join(bytes(s) for s in r)).digest() for r in reqs]\n"
+        "    got = e.hash_slices(reqs, dedup=True)\n"
+        "    assert [r.tobytes() for r in got] == want, seed\n"
+        "    assert e.last_unique == t.python_plan(reqs)[1], seed\n"
+        "    tk = e.submit_slices(reqs, dedup=True)\n"
+        "    assert [r.tobytes() for r in e.wait(tk)] == want, seed\n"
+        "e.close()\n"
+        "print('ok')\n" % (root, os.path.join(root, "tests"))
+    )
+    env = dict(os.environ, MIRSHA_DEDUP_WEAK_FP="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
