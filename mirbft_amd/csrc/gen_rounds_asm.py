@@ -58,16 +58,21 @@ def op(i):
 COMPLEX = ("v_alignbit_b32", "v_add3_u32", "v_bfi_b32")
 
 
-def yield_after_complex(lines):
-    out = []
+def yield_after_complex(lines, which=COMPLEX, every=1):
+    """An issue-yield s_nop 0 after every `every`-th op whose opcode is in `which`."""
+    out, k = [], 0
     for ln in lines:
         out.append(ln)
-        if ln.split()[0] in COMPLEX:
-            out.append("s_nop 0")
+        if ln.split()[0] in which:
+            k += 1
+            if k % every == 0:
+                out.append("s_nop 0")
     return out
 
 
 def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr", nops=False):
+    """nops: False, True (after every 4-cycle op) or (opcodes, every) for
+    A/B yield patterns."""
     """8 rounds from j0.  k_mode: "sgpr" = K[j] as 8 SGPR inputs %28..%35 (the
     compiler hoists all 64 constants out of a block loop: 64 live SGPRs);
     "smov" = K[j] written by s_mov_b32 into ONE scratch SGPR output %28 inside
@@ -127,13 +132,15 @@ def block(j0, ch_mode="bfi", add_mode="add3", k_mode="sgpr", nops=False):
             lines.append(f"v_add3_u32 {h}, {h}, {t0}, {t1}")
         else:
             lines += [f"v_add_u32_e32 {h}, {h}, {t0}", f"v_add_u32_e32 {h}, {h}, {t1}"]
-        if nops:
+        if nops is True:
             lines = yield_after_complex(lines)
+        elif nops:
+            lines = yield_after_complex(lines, *nops)
         if k_mode == "smov":
             # K[j] into the scratch SGPR: in the slot of the round's first
             # yield with nops (after its first 4-cycle op), else up front.
             mov = f"s_mov_b32 {op(KOP[0])}, 0x{K[j]:08x}"
-            if nops:
+            if "s_nop 0" in lines:
                 lines[lines.index("s_nop 0")] = mov
             else:
                 lines.insert(0, mov)
@@ -254,12 +261,24 @@ def emit_fn_kw(name):
 # the latency form of the lone-wave chains.
 VARIANTS = {
     # name: (ch_mode, add_mode, k_mode, nops)
-    "rounds_asm": ("bitop3", "add3", "smov", True),
+    # request-kernel form: a yield after every SECOND 4-cycle op (the register
+    # loop alone prefers one after every op, 5,021 vs 5,090 cycles per
+    # wave-compression, but in the request kernel -- memory stalls, progress
+    # priorities -- every second one measured 187.8-188.1 vs 189.1-189.5 us per
+    # config-2 launch on two boxes, profiles/r02y)
+    "rounds_asm": ("bitop3", "add3", "smov", (COMPLEX, 2)),
     "rounds_asm_nonop": ("bitop3", "add3", "sgpr", False),
 }
 # A/B forms for tools/ only (tools/sha256_rounds_asm_ab.h), bit-identical.
 AB_VARIANTS = {
     "rounds_asm_ksgpr": ("bitop3", "add3", "sgpr", True),
+    # yield patterns (A/B against the product's "after every second 4-cycle op")
+    "rounds_asm_y_every": ("bitop3", "add3", "smov", True),  # the round-1/2 product form
+    "rounds_asm_y_rot": ("bitop3", "add3", "smov", (("v_alignbit_b32",), 1)),
+    "rounds_asm_y_add3": ("bitop3", "add3", "smov", (("v_add3_u32",), 1)),
+    "rounds_asm_y_third": ("bitop3", "add3", "smov", (COMPLEX, 3)),
+    "rounds_asm_y_quarter": ("bitop3", "add3", "smov", (COMPLEX, 4)),
+    "rounds_asm_y_rothalf": ("bitop3", "add3", "smov", (("v_alignbit_b32",), 2)),
     "rounds_asm_bfi": ("bfi", "add3", "sgpr", False),
     "rounds_asm_add2": ("bitop3", "add", "sgpr", False),
     "rounds_asm_lit": ("bitop3", "add3", "lit", False),

@@ -8,7 +8,7 @@
 #include <stdint.h>
 
 #include "sha256_rounds_asm.h"
-#ifdef MIRSHA_AB_KSGPR  // A/B build only (tools/ab_build.sh): round-1 form, K in 8 SGPR inputs per statement
+#if defined(MIRSHA_AB_KSGPR) || defined(MIRSHA_AB_ROUNDS)  // A/B builds only (tools/ab_build.sh)
 #include "sha256_rounds_asm_ab.h"
 #endif
 
@@ -77,7 +77,7 @@ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
 // The same compression with the 64 rounds in generated gfx950 assembly
 // (sha256_rounds_asm.h): a..h + W[16] + 4 temporaries, no compiler-hoisted
 // schedule partial sums.  Throughput form: an issue-yield `s_nop 0` after
-// every 4-cycle-class op (-8.7 % cycles at 4-8 waves/SIMD, gen_rounds_asm.py);
+// every second 4-cycle-class op (gen_rounds_asm.py, VARIANTS);
 // the round constants are written into one scratch SGPR inside the asm, so a
 // block loop keeps no 64 constant SGPRs live (SGPR count sets the waves per
 // SIMD: MI355X_MICROARCH.md, residency).
@@ -85,8 +85,10 @@ __device__ __forceinline__ void compress_asm(uint32_t st[8], uint32_t w[16]) {
     uint32_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = st[i];
-#ifdef MIRSHA_AB_KSGPR
+#if defined(MIRSHA_AB_KSGPR)
     rounds_asm_ksgpr(s, w);
+#elif defined(MIRSHA_AB_ROUNDS)  // e.g. -DMIRSHA_AB_ROUNDS=rounds_asm_y_rot
+    MIRSHA_AB_ROUNDS(s, w);
 #else
     rounds_asm(s, w);
 #endif

@@ -12,6 +12,8 @@
 #   occ6:      -DMIRSHA_AB_OCC6         (request kernel held to 6 waves/SIMD by LDS)
 #   pf5:       -DMIRSHA_AB_PREFETCH     (next block chunks prefetched into registers, 5 waves/SIMD)
 #   spawn:     -DMIRSHA_AB_SPAWN_THREADS (host passes on threads spawned per call instead of the pool)
+#   yevery:    -DMIRSHA_AB_ROUNDS=rounds_asm_y_every (issue-yield s_nop after every 4-cycle op,
+#              the round-1/2 form; other patterns: rounds_asm_y_* in tools/sha256_rounds_asm_ab.h)
 #   prioN:     -DMIRSHA_PRIO_TOP=N      (block b's rounds at issue priority max(0, N - b), clamped to 3; product 3)
 set -euo pipefail
 cd "$(dirname "$0")/.."
@@ -32,6 +34,6 @@ build occ6 -DMIRSHA_AB_OCC6 &
 build pf5 -DMIRSHA_AB_PREFETCH &
 build spawn -DMIRSHA_AB_SPAWN_THREADS &
 build prio0 -DMIRSHA_PRIO_TOP=0 &
-build prio4 -DMIRSHA_PRIO_TOP=4 &
+build yevery -DMIRSHA_AB_ROUNDS=rounds_asm_y_every &
 wait
 ls -la tools/scratch/*/libmirsha.so
