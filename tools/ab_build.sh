@@ -14,12 +14,14 @@
 #   spawn:     -DMIRSHA_AB_SPAWN_THREADS (host passes on threads spawned per call instead of the pool)
 #   yevery:    -DMIRSHA_AB_ROUNDS=rounds_asm_y_every (issue-yield s_nop after every 4-cycle op,
 #              the round-1/2 form; other patterns: rounds_asm_y_* in tools/sha256_rounds_asm_ab.h)
+#   AB_ONLY="a b" builds only the named variants.
 #   prioN:     -DMIRSHA_PRIO_TOP=N      (block b's rounds at issue priority max(0, N - b), clamped to 3; product 3)
 set -euo pipefail
 cd "$(dirname "$0")/.."
 SRC=mirbft_amd/csrc
 build() {
     local name=$1; shift
+    if [ -n "${AB_ONLY:-}" ] && [[ " $AB_ONLY " != *" $name "* ]]; then return 0; fi
     mkdir -p tools/scratch/$name
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Itools "$@" -shared \
         -o tools/scratch/$name/libmirsha.so $SRC/mirsha_kernels.hip $SRC/mirsha_api.hip $SRC/mirsha_scan.hip $SRC/mirsha_host.cpp
