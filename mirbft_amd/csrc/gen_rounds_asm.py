@@ -242,6 +242,131 @@ def block_kw():
     return lines
 
 
+def tail_round(j):
+    """Round j of a FINAL block whose words 4..15 are wave-uniform constants:
+    W4 = c4 (0x80000000 when the block holds exactly 16 message bytes, else 0),
+    W5..W13 = 0, W14 = c14, W15 = c15 (the 64-bit bit length).  Only W0..W3
+    come from the message.  Constant terms of the schedule arrive summed in
+    SGPRs (cs16 = s1(c14), cs17 = s1(c15), cs19 = s0(c4), cs29 = s0(c14),
+    cs30 = s0(c15) + c14) and the rounds 4..15 add K[j] + W[j] as one scalar
+    (kw4, kw14, kw15, or K[j] itself): 89 instead of 160 schedule ops and 12
+    two-input adds instead of v_add3.  Named operands (%[x])."""
+    a, b, c, d, e, f, g, h = [f"%[s{(k - j) % 8}]" for k in range(8)]
+    W = lambda i: f"%[w{i & 15}]"
+    t0, t1, t2, t3 = "%[t0]", "%[t1]", "%[t2]", "%[t3]"
+    s0 = lambda x: [f"v_alignbit_b32 {t0}, {x}, {x}, 7", f"v_alignbit_b32 {t1}, {x}, {x}, 18",
+                    f"v_lshrrev_b32_e32 {t2}, 3, {x}", f"v_bitop3_b32 {t0}, {t0}, {t1}, {t2} bitop3:0x96"]
+    s1 = lambda x: [f"v_alignbit_b32 {t1}, {x}, {x}, 17", f"v_alignbit_b32 {t2}, {x}, {x}, 19",
+                    f"v_lshrrev_b32_e32 {t3}, 10, {x}", f"v_bitop3_b32 {t1}, {t1}, {t2}, {t3} bitop3:0x96"]
+    wj = W(j)
+    lines = []
+    if j == 16:
+        lines += s0(W(1)) + [f"v_add3_u32 {wj}, {wj}, {t0}, %[cs16]"]
+    elif j == 17:
+        lines += s0(W(2)) + [f"v_add3_u32 {wj}, {wj}, {t0}, %[cs17]"]
+    elif j == 18:  # + W11 = 0
+        lines += s0(W(3)) + s1(W(16)) + [f"v_add3_u32 {wj}, {wj}, {t0}, {t1}"]
+    elif j == 19:  # + W12 = 0, s0(W4) = cs19
+        lines += s1(W(17)) + [f"v_add3_u32 {wj}, {wj}, {t1}, %[cs19]"]
+    elif j in (20, 21, 22):  # s1(W[j-2]) + W4 / W14 / W15 (the other terms are zero)
+        lines += s1(W(j - 2)) + [f"v_add_u32_e32 {wj}, %[{('c4', 'c14', 'c15')[j - 20]}], {t1}"]
+    elif 23 <= j <= 28:  # s1(W[j-2]) + W[j-7]
+        lines += s1(W(j - 2)) + [f"v_add_u32_e32 {wj}, {W(j - 7)}, {t1}"]
+    elif j in (29, 30):  # + s0(W14) / s0(W15) + W14
+        lines += s1(W(j - 2)) + [f"v_add3_u32 {wj}, {W(j - 7)}, {t1}, %[cs{j}]"]
+    elif j == 31:  # s1(W29) + W24 + s0(W16) + W15
+        lines += s0(W(16)) + s1(W(29)) + [f"v_add3_u32 {wj}, {W(24)}, {t0}, {t1}",
+                                            f"v_add_u32_e32 {wj}, %[c15], {wj}"]
+    lines += [
+        f"v_alignbit_b32 {t0}, {e}, {e}, 6",
+        f"v_alignbit_b32 {t1}, {e}, {e}, 11",
+        f"v_alignbit_b32 {t2}, {e}, {e}, 25",
+        f"v_bitop3_b32 {t0}, {t0}, {t1}, {t2} bitop3:0x96",
+        f"v_bitop3_b32 {t1}, {e}, {f}, {g} bitop3:0xca",
+        f"v_add3_u32 {h}, {h}, {t0}, {t1}",
+    ]
+    kmov = None
+    if j < 4 or j >= 16:
+        lines.append(f"v_add3_u32 {h}, {h}, %[kt], {wj}")
+        kmov = f"s_mov_b32 %[kt], 0x{K[j]:08x}"
+    elif j in (4, 14, 15):
+        lines.append(f"v_add_u32_e32 {h}, %[kw{j}], {h}")
+    else:  # W[j] = 0
+        lines.append(f"v_add_u32_e32 {h}, %[kt], {h}")
+        kmov = f"s_mov_b32 %[kt], 0x{K[j]:08x}"
+    lines += [
+        f"v_add_u32_e32 {d}, {d}, {h}",
+        f"v_alignbit_b32 {t0}, {a}, {a}, 2",
+        f"v_alignbit_b32 {t1}, {a}, {a}, 13",
+        f"v_alignbit_b32 {t2}, {a}, {a}, 22",
+        f"v_bitop3_b32 {t0}, {t0}, {t1}, {t2} bitop3:0x96",
+        f"v_bitop3_b32 {t1}, {a}, {b}, {c} bitop3:0xe8",
+        f"v_add3_u32 {h}, {h}, {t0}, {t1}",
+    ]
+    lines = yield_after_complex(lines, COMPLEX, 2)
+    if kmov:
+        if "s_nop 0" in lines:
+            lines[lines.index("s_nop 0")] = kmov
+        else:
+            lines.insert(0, kmov)
+    return lines
+
+
+# statements of the tail form: (first round, end round); the window words each
+# one touches are derived from its text (at most 29 operands per statement)
+TAIL_STATEMENTS = [(0, 8), (8, 16), (16, 24), (24, 28), (28, 32)]
+TAIL_SCALARS = ["kw4", "kw14", "kw15", "c4", "c14", "c15", "cs16", "cs17", "cs19", "cs29", "cs30"]
+
+
+def emit_fn_tail(name, normal_variant):
+    ch, ad, km, nops = VARIANTS[normal_variant]
+    out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16], const TailWords& k) {{",
+           "    uint32_t t0, t1, t2, t3; uint32_t kt;"]
+    import re
+    defined = {f"w{i}" for i in range(4)}  # window words 4..15 are first WRITTEN (W20..W31)
+    for j0, j1 in TAIL_STATEMENTS:
+        body = []
+        for j in range(j0, j1):
+            body += tail_round(j)
+        text = "\n".join(body)
+        used = set(re.findall(r"%\[(\w+)\]", text))
+        fresh = set()  # words whose first access in this statement is a write: "=&v"
+        for ln in body:
+            names = re.findall(r"%\[(w\d+)\]", ln)
+            for k, nm in enumerate(names):
+                if nm in defined or nm in fresh:
+                    continue
+                assert k == 0 and ln.split(None, 1)[1].startswith(f"%[{nm}]"), f"{nm} read before written"
+                fresh.add(nm)
+        defined |= fresh
+        out.append(f"    // rounds {j0}..{j1 - 1} (final-block form)")
+        out.append("    asm volatile(")
+        for ln in body:
+            out.append(f'        "{ln}\\n\\t"')
+        outs = [f'[s{i}] "+v"(s[{i}])' for i in range(8)]
+        outs += [f'[w{i}] "{"=&v" if f"w{i}" in fresh else "+v"}"(w[{i}])' for i in range(16) if f"w{i}" in used]
+        outs += [f'[t{i}] "=&v"(t{i})' for i in range(4) if f"t{i}" in used]
+        if "kt" in used:
+            outs.append('[kt] "=&s"(kt)')
+        ins = [f'[{x}] "s"(k.{x})' for x in TAIL_SCALARS if x in used]
+        out.append(f"        : {', '.join(outs)}")
+        out.append(f"        : {', '.join(ins)});")
+    # rounds 32..63: the ordinary statements (every window word is live)
+    for j0 in range(32, 64, 8):
+        body = block(j0, ch, ad, km, nops)
+        out.append(f"    // rounds {j0}..{j0 + 7}")
+        out.append("    asm volatile(")
+        for ln in body:
+            out.append(f'        "{ln}\\n\\t"')
+        outs = ", ".join([f'"+v"(s[{i}])' for i in range(8)] + [f'"+v"(w[{i}])' for i in range(16)]
+                         + ['"=&v"(t0)', '"=&v"(t1)', '"=&v"(t2)', '"=&v"(t3)', '"=&s"(kt)'])
+        out.append(f"        : {outs}")
+        out.append("        : );")
+    out.append("}")
+    out.append("")
+    return out
+
+
 def emit_fn_kw(name):
     out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint4 k0, uint4 k1) {{",
            "    uint32_t t0, t1, t2, t3, t4, t5;",
@@ -330,6 +455,17 @@ def emit():
     ]
     for name, (ch, ad, km, nops) in VARIANTS.items():
         out += emit_fn(name, ch, ad, km, nops)
+    out += [
+        "// Wave-uniform constants of a final block whose words 4..15 are padding",
+        "// (rounds_asm_tail; filled by tail_words() in sha256_device.h).",
+        "struct TailWords {",
+        "    uint32_t " + ", ".join(TAIL_SCALARS) + ";",
+        "};",
+        "// rounds_asm for a final block with only W0..W3 from the message (same",
+        "// yield pattern): the schedule's constant terms and K[j] + W[j] of rounds",
+        "// 4..15 are scalars (71 fewer schedule ops; 12 v_add3 become v_add).",
+    ]
+    out += emit_fn_tail("rounds_asm_tail", "rounds_asm")
     out.append("// 8 consumer rounds with K + W precomputed (pair kernels): names rotate")
     out.append("// back after 8 rounds, so the same statement serves every 8-round chunk.")
     out += emit_fn_kw("rounds_kw8_asm")

@@ -36,6 +36,8 @@ uint32_t pair_max_groups();
 // Arenas up to kMaxBufferArena bytes use one 32-bit buffer descriptor; larger
 // ones (any size) the 64-bit per-lane addressed loader.
 constexpr uint64_t kMaxBufferArena = 0xFFFFFF00ull;
+// ... and digests through one descriptor (32-bit offsets 32 i) up to 2^27 messages.
+constexpr uint32_t kMaxBufferMsgs = 1u << 27;
 // off[i] = len[0] + ... + len[i-1] (exclusive scan; mirsha_scan.hip).  With
 // tmp == nullptr only sets tmp_bytes (the scratch size for n requests).
 hipError_t launch_offsets_scan(void* tmp, size_t& tmp_bytes, const uint32_t* len, uint64_t* off, uint32_t n,

@@ -143,9 +143,12 @@ __device__ __forceinline__ void pad_words(uint32_t p, uint32_t L, bool last_bloc
 // The same padding for a whole block of 16 words when the block position
 // soff, the length L and `last` are wave-uniform (SGPRs): the keep / mark
 // words are scalar, one v_bitop3 per word.
+// kWords < 16: only the first kWords words (the final-block tail form keeps
+// the rest, and the bit length, as scalars).
+template <int kWords = 16>
 __device__ __forceinline__ void pad_block_uniform(uint32_t w[16], uint32_t soff, uint32_t L, bool last) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
+    for (int k = 0; k < kWords; k++) {
         const int32_t t = (int32_t)(L - (soff + 4u * k));  // message bytes left at word k
         const uint32_t sh = (uint32_t)t << 3;              // only used when 0 <= t <= 3
         uint32_t keep = t >= 4 ? 0xFFFFFFFFu : (t <= 0 ? 0u : ~(0xFFFFFFFFu >> sh));
@@ -178,6 +181,17 @@ __device__ __forceinline__ void store_digest(uint8_t* out, uint32_t msg, const u
                       __builtin_bswap32(st[3]));
     d[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
                       __builtin_bswap32(st[7]));
+}
+
+__device__ __forceinline__ void store_digest_buf(__amdgpu_buffer_rsrc_t ors, uint32_t msg, const uint32_t st[8]) {
+    __builtin_amdgcn_raw_buffer_store_b128(
+        (uint32_t __attribute__((ext_vector_type(4)))){__builtin_bswap32(st[0]), __builtin_bswap32(st[1]),
+                                                        __builtin_bswap32(st[2]), __builtin_bswap32(st[3])},
+        ors, 32u * msg, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(
+        (uint32_t __attribute__((ext_vector_type(4)))){__builtin_bswap32(st[4]), __builtin_bswap32(st[5]),
+                                                        __builtin_bswap32(st[6]), __builtin_bswap32(st[7])},
+        ors, 32u * msg + 16u, 0, 0);
 }
 
 // Digest store with the sc1 cache policy: written through to memory (the line
@@ -349,6 +363,15 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #else
         const bool uni = wave_max(valid ? L : 0u) == min_l;
 #endif
+        // Final-block tail form (compress_asm_tail) for uniform tiles whose
+        // final block holds at most 16 message bytes; its scalars up front.
+        const int32_t u_last = (int32_t)(min_l - 64u * (wave_nb - 1u));
+#ifdef MIRSHA_AB_NOTAIL  // A/B build only: every block through compress_asm
+        const bool tail_ok = false;
+#else
+        const bool tail_ok = uni && u_last <= 16;
+#endif
+        const TailWords tw = tail_words(u_last, min_l);
         uint32_t vo[4], sel[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -368,8 +391,15 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             }
         }
 #endif
-        for (uint32_t blk = 0; blk < wave_nb; blk++) {
+        // One block of the tile into w[] (lane = message): loads, big-endian
+        // words, per-chunk padding of mixed tiles, the LDS transpose.
+        // trim (the tail-form final block): chunks wholly past the tile's
+        // length are not loaded (zeros; words 4..15 are never read there),
+        // so a config-2 request's final block fetches its 16 bytes, not 64.
+        auto stage = [&](uint32_t blk, uint32_t w[16], uint32_t ln, bool trim) {
             const uint32_t soff = 64u * blk;
+            const uint32_t qq = ln & 3u;
+            const bool skip = trim && soff + 16u * qq >= min_l;
             RawChunk rc[4];
 #ifdef MIRSHA_AB_PREFETCH
             if (pf) {
@@ -387,7 +417,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                 }
             } else
 #endif
-            if (far) {
+            if (far && !trim) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], soff, 0);
@@ -399,9 +429,19 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                     for (int j = 0; j < 4; j++)
                         rc[j].v[4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo[j], soff + 16u, 0);
                 }
+            } else if (far) {
+                // a skipped chunk reads past the descriptor's range: zeros, no access
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t a = skip ? 0xFFFFFFE0u : vo[j] + soff;
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, a, 0, 0);
+                    rc[j].v[0] = v[0]; rc[j].v[1] = v[1]; rc[j].v[2] = v[2]; rc[j].v[3] = v[3];
+                    rc[j].v[4] = aligned ? 0u : __builtin_amdgcn_raw_buffer_load_b32(rsrc, a + 16u, 0, 0);
+                }
             } else {
 #pragma unroll
-                for (int j = 0; j < 4; j++) issue_chunk(rsrc, (uint32_t)records, vo[j] + soff, 0u, 0u, true, rc[j]);
+                for (int j = 0; j < 4; j++)
+                    issue_chunk(rsrc, (uint32_t)records, vo[j] + soff, 0u, 0u, !skip, rc[j]);
             }
             const bool pad = soff + 64u > min_l;  // wave-uniform
 #pragma unroll
@@ -411,36 +451,67 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                 for (int k = 0; k < 4; k++) wq[k] = be_word(rc[j].v[k + 1], rc[j].v[k], sel[j]);
                 if (pad && !uni) {
                     // Lengths fetched here (rare blocks), not kept live across the rounds.
-                    const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(lane >> 2), 64);
-                    pad_words(soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
+                    const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(ln >> 2), 64);
+                    pad_words(soff + 16u * qq, Lm, blk + 1u == blocks_for_len(Lm), qq, wq);
                 }
                 // Unconditional: a slot of a finished message is never read.
-                my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+                my[lds_slot(16u * j + (ln >> 2), qq)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
             }
             // Cross-lane hand-off inside one wave: LDS ops of a wave execute
             // in order; the fences only stop the compiler from reordering.
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            uint32_t w[16];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+                const uint4 x = my[lds_slot(ln, (uint32_t)k)];
                 w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (pad && uni) {
-                // (through an opaque s_mov: hipcc otherwise peels the loop's
-                // last iteration to fold the test, a third copy of the rounds)
-                uint32_t left;
-                asm volatile("s_sub_u32 %0, %1, %2" : "=s"(left) : "s"(wave_nb), "s"(blk));
-                pad_block_uniform(w, soff, min_l, left == 1u);
+        };
+        // A uniform tile's tail-form final block runs after the loop, not as a
+        // branch inside it: two round copies joined inside the loop made the
+        // register allocator spill (64 VGPRs is the 8-wave budget).
+        const uint32_t loop_nb = tail_ok ? wave_nb - 1u : wave_nb;
+        for (uint32_t blk = 0; blk < loop_nb; blk++) {
+            const uint32_t soff = 64u * blk;
+            uint32_t w[16];
+            stage(blk, w, lane, false);
+            if (soff + 64u > min_l && uni) {  // wave-uniform
+                // (the block count through an opaque s_mov: hipcc otherwise
+                // peels the loop's last iteration to fold the test, a third
+                // copy of the rounds.  An s_mov, not the s_sub_u32 of before:
+                // SALU arithmetic writes SCC behind the compiler's back, and a
+                // padding mask's s_cselect read the clobbered SCC -- a wrong
+                // 0x80 marker at length 60, tests/test_gpu_parity.py uniform tiles)
+                uint32_t wnb;
+                asm volatile("s_mov_b32 %0, %1" : "=s"(wnb) : "s"(wave_nb));
+                pad_block_uniform(w, soff, min_l, wnb - blk == 1u);
             }
             progress_prio(blk);
             if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm(st, w);
+        }
+        // Final block of a uniform tile holding at most 16 message bytes
+        // (u <= 16; u < 0: the length-only block after a full one): words
+        // 4..15 are padding constants, and the tail rounds take them, and the
+        // schedule terms they feed, as scalars (requests of a 16-byte header
+        // plus a 2^k-byte payload: BASELINE configs 2 and 3).
+        if (tail_ok) {
+            const uint32_t blk = wave_nb - 1u;
+            uint32_t w[16];
+            // (the lane index through an opaque copy: the LDS slot addresses
+            // are then recomputed here instead of kept live, and spilled,
+            // across the loop)
+            uint32_t ln;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+            stage(blk, w, ln, true);
+            pad_block_uniform<4>(w, 64u * blk, min_l, false);
+            progress_prio(blk);
+            if (blk == 0u) MIRSHA_STAMP(t, 2);
+            if (blk < nb) compress_asm_tail(st, w, tw);
         }
         MIRSHA_STAMP_END(t);
     } else if constexpr (kLds) {
@@ -496,7 +567,18 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             if (active) compress_asm(st, w);
         }
     }
-    if (valid) store_digest(out, msg, st);
+    if (valid) {
+        if constexpr (kLds && !kWide) {
+            // 32-bit buffer offsets (launch_msgs sends n >= 2^27 to the wide
+            // form): the message index stays one VGPR across the block loop
+            // instead of a 64-bit address pair (the tail form spilled it).
+            const __amdgpu_buffer_rsrc_t ors =
+                __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, (int)(32u * n), 0x00020000);
+            store_digest_buf(ors, msg, st);
+        } else {
+            store_digest(out, msg, st);
+        }
+    }
 }
 
 // One wave per workgroup: a workgroup's slot and LDS are released only when
@@ -1363,7 +1445,7 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
     const uint32_t tiles = (n + 63u) / 64u;
     const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
     const uint32_t mgrid = (tiles + kMsgWaves - 1u) / kMsgWaves;
-    if (arena_len > kMaxBufferArena) {  // 64-bit per-lane addressing (LDS loader)
+    if (arena_len > kMaxBufferArena || n >= kMaxBufferMsgs) {  // 64-bit addressing (LDS loader)
         sha256_msgs_kernel<true, true><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }

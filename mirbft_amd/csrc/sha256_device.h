@@ -96,6 +96,40 @@ __device__ __forceinline__ void compress_asm(uint32_t st[8], uint32_t w[16]) {
     for (int i = 0; i < 8; i++) st[i] += s[i];
 }
 
+// The wave-uniform scalars of a final block whose words 4..15 are all padding
+// (FIPS 180-4 §5.1.1): u = message bytes in the block (at most 16; negative
+// for the length-only block that follows a block ending in the 0x80 marker),
+// L = message length.  Every field is passed through v_readfirstlane: the
+// rotates have no scalar form and would otherwise stay VALU results, which
+// the compiler hoists out of the block loop into VGPRs (the request kernel
+// then spilled); called once per tile, before the loop.
+__device__ __forceinline__ TailWords tail_words(int32_t u, uint32_t L) {
+    auto sgpr = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+    TailWords k;
+    k.c4 = u == 16 ? 0x80000000u : 0u;
+    k.c14 = L >> 29;
+    k.c15 = L << 3;
+    k.kw4 = kK[4] + k.c4;
+    k.kw14 = kK[14] + k.c14;
+    k.kw15 = kK[15] + k.c15;
+    k.cs16 = sgpr(ssig1(k.c14));
+    k.cs17 = sgpr(ssig1(k.c15));
+    k.cs19 = sgpr(ssig0(k.c4));
+    k.cs29 = sgpr(ssig0(k.c14));
+    k.cs30 = sgpr(ssig0(k.c15) + k.c14);
+    return k;
+}
+
+// compress_asm for such a final block: only w[0..3] are read (already padded).
+__device__ __forceinline__ void compress_asm_tail(uint32_t st[8], uint32_t w[16], const TailWords& k) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = st[i];
+    rounds_asm_tail(s, w, k);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] += s[i];
+}
+
 // Latency form (no yields) for digest-list chains, which run at most one
 // wave per SIMD: there the yields only lengthen the chain.
 __device__ __forceinline__ void compress_asm_lat(uint32_t st[8], uint32_t w[16]) {

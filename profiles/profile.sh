@@ -23,5 +23,6 @@ timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex sha256 --o
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex sha256 --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py "${PARGS[@]}" > "$OUT/pmc_write.log" 2>&1
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex sha256 --output-format csv -d "$OUT/pmc_sq" -o run -- python3 bench.py "${PARGS[@]}" > "$OUT/pmc_sq.log" 2>&1
 timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_VMEM TCC_HIT_sum TCC_MISS_sum --kernel-include-regex sha256 --output-format csv -d "$OUT/pmc_mem" -o run -- python3 bench.py "${PARGS[@]}" > "$OUT/pmc_mem.log" 2>&1 || echo "pmc_mem pass failed (counter names?)" >> "$OUT/notes.txt"
+timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --kernel-include-regex sha256 --output-format csv -d "$OUT/pmc_size" -o run -- python3 bench.py "${PARGS[@]}" > "$OUT/pmc_size.log" 2>&1
 python3 profiles/summarize.py "$OUT" > "$OUT/summary.json"
 echo done

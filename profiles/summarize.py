@@ -1,8 +1,17 @@
 #!/usr/bin/env python3
 """Summarize a profiles/profile.sh output directory: per-kernel average
-duration (kernel trace) and per-launch PMC counter averages, with the gfx950
-corrections of MI355X_MICROARCH.md §HBM (FETCH_SIZE x2 for wide streaming
-reads; WRITE_SIZE as read) and the effective clock GRBM_GUI_ACTIVE / 8 / time."""
+duration (kernel trace) and per-launch PMC counter averages, and the L2
+memory-side bytes per launch.
+
+Read bytes come from the size-split request counters when that pass exists:
+32 x TCC_EA0_RDREQ_32B + 64 x TCC_EA0_RDREQ_64B + 128 x TCC_EA0_RDREQ_128B.
+rocprofv3's FETCH_SIZE on gfx950 counts every non-32-B request as 64 B (its
+128-B term reads TCC_BUBBLE, which stays 0 here), hence MI355X_MICROARCH.md
+§HBM's "x2" for wide streaming reads, which are all 128-B requests; the
+request kernel's loads mix 64-B and 128-B requests, so neither x1 nor x2 is
+right for it (profiles/r02ac: calibration kernels and the request kernel).
+Without that pass the FETCH_SIZE x 2 upper bound is used.  WRITE_SIZE as read;
+effective clock GRBM_GUI_ACTIVE / 8 / time."""
 import collections
 import csv
 import json
@@ -40,7 +49,7 @@ def main(d):
             v.sort()
             out["kernels"].setdefault(k, {}).setdefault("by_grid", {})[str(g)] = {
                 "launches": len(v), "mean_us": sum(v) / len(v), "median_us": v[len(v) // 2]}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mem"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_mem", "pmc_size"):
         f = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(f):
             continue
@@ -53,12 +62,17 @@ def main(d):
             out["kernels"].setdefault(k, {})[c] = sum(v) / len(v)
     for k, v in out["kernels"].items():
         t = v.get("avg_ns")
+        sized = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+        if all(c in v for c in sized):
+            v["hbm_read_bytes_sized"] = 32 * v[sized[0]] + 64 * v[sized[1]] + 128 * v[sized[2]]
         if "FETCH_SIZE" in v:
-            v["hbm_read_bytes_corrected"] = v["FETCH_SIZE"] * 1024 * 2  # KB units, x2 gfx950 correction
+            v["hbm_read_bytes_upper"] = v["FETCH_SIZE"] * 1024 * 2  # KB units, every request taken as 128 B
         if "WRITE_SIZE" in v:
             v["hbm_write_bytes"] = v["WRITE_SIZE"] * 1024
-        if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
-            v["hbm_bytes_per_launch"] = v["hbm_read_bytes_corrected"] + v["hbm_write_bytes"]
+        rd = v.get("hbm_read_bytes_sized", v.get("hbm_read_bytes_upper"))
+        if rd is not None and "WRITE_SIZE" in v:
+            v["hbm_bytes_per_launch"] = rd + v["hbm_write_bytes"]
+            v["hbm_read_method"] = "sized requests" if "hbm_read_bytes_sized" in v else "FETCH_SIZE x 2 (upper bound)"
         if t and "GRBM_GUI_ACTIVE" in v:
             v["effective_clock_ghz"] = v["GRBM_GUI_ACTIVE"] / 8 / t
         if "SQ_WAVE_CYCLES" in v:

@@ -3,9 +3,11 @@
 keyed by bench.kernel_source_key(variant) (sha256 of the device sources), so
 bench.py reports `roofline.traffic` only for the exact kernel it ran.
 
-HBM bytes per launch = FETCH_SIZE x 1024 x 2 + WRITE_SIZE x 1024 (KB units;
-gfx950 FETCH_SIZE counts half the bytes of wide streaming reads,
-MI355X_MICROARCH.md §HBM), averaged over every launch of the kernel in the pass.
+L2 memory-side bytes per launch = read bytes from the size-split request
+counters (32 x TCC_EA0_RDREQ_32B + 64 x _64B + 128 x _128B; see
+profiles/summarize.py: rocprofv3's FETCH_SIZE takes every request as 64 B on
+gfx950) + WRITE_SIZE x 1024, averaged over every launch of the kernel in the
+pass; FETCH_SIZE x 2 (upper bound) when the size pass is missing.
 
 Usage: update_traffic.py <summary.json> --tag r02 [--config 2] [--variant 0] [--kernel sha256_msgs_kernel]
 """
@@ -33,7 +35,10 @@ def main():
     entry = {
         "key": kernel_source_key(a.variant), "config": a.config, "variant": a.variant, "kernel": a.kernel,
         "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],
+        "read_method": k.get("hbm_read_method"),
         "FETCH_SIZE_kb": k.get("FETCH_SIZE"), "WRITE_SIZE_kb": k.get("WRITE_SIZE"),
+        "TCC_EA0_RDREQ_32B_sum": k.get("TCC_EA0_RDREQ_32B_sum"), "TCC_EA0_RDREQ_64B_sum": k.get("TCC_EA0_RDREQ_64B_sum"),
+        "TCC_EA0_RDREQ_128B_sum": k.get("TCC_EA0_RDREQ_128B_sum"),
         "TCC_HIT_sum": k.get("TCC_HIT_sum"), "TCC_MISS_sum": k.get("TCC_MISS_sum"),
         "source": f"{a.summary} (profiles/profile.sh {a.tag})",
     }
@@ -47,8 +52,9 @@ def main():
     entries = [e for e in tf.get("entries", [])
                if not (e.get("key") == entry["key"] and e.get("config") == entry["config"])]
     entries.append(entry)
-    out = {"method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes over bench.py; bytes = "
-                     "FETCH_SIZE*1024*2 + WRITE_SIZE*1024 per launch (MI355X_MICROARCH.md §HBM)",
+    out = {"method": "rocprofv3 --pmc passes over bench.py (profiles/profile.sh); bytes per launch = "
+                     "32*TCC_EA0_RDREQ_32B + 64*TCC_EA0_RDREQ_64B + 128*TCC_EA0_RDREQ_128B + WRITE_SIZE*1024 "
+                     "(entries without read_method 'sized requests': FETCH_SIZE*1024*2 + WRITE_SIZE*1024)",
            "entries": entries}
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(entry, indent=1))

@@ -85,6 +85,25 @@ def test_every_length_0_to_600_every_alignment(eng):
     assert _hex(got) == [hashlib.sha256(m).hexdigest() for m in msgs]
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3], ids=["aligned", "shift1", "shift3"])
+def test_uniform_tiles_every_length_tail_form(eng, shift):
+    """Tiles whose messages share one length: the FIPS padding after the LDS
+    transpose and, when the final block holds <= 16 message bytes (or only the
+    bit length), the tail-form rounds with trimmed loads.  71 messages per
+    length (a full tile + a partial one), packed back to back from a base of
+    `shift` bytes and ending exactly at the arena end (range-checked loads)."""
+    rng = np.random.default_rng(40 + shift)
+    for L in range(0, 331):
+        n = 71
+        arena = rng.integers(0, 256, shift + n * L, dtype=np.uint8)
+        off = shift + np.arange(n, dtype=np.uint64) * L
+        lens = np.full(n, L, dtype=np.uint32)
+        got = eng.hash_batch(arena, off, lens)
+        raw = arena.tobytes()
+        want = [hashlib.sha256(raw[shift + i * L: shift + (i + 1) * L]).digest() for i in range(n)]
+        assert [r.tobytes() for r in got] == want, f"length {L}"
+
+
 def test_mixed_buckets_origin_order(eng):
     """Lengths spanning 1..1000 blocks go through the bucketing permutation;
     digests must still come back at their origin index."""
