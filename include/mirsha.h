@@ -270,9 +270,11 @@ int mirsha_pipeline_mode(const mirsha_pipeline* p);
 int mirsha_pipeline_status(mirsha_ctx* ctx, mirsha_pipeline* p);
 /* Diagnostics of a fused plan created with MIRSHA_FUSED_TRACE=1 in the
  * environment: the last run's timeline (s_memrealtime ticks, 100 MHz) --
- * per tile [start, end] at [2t, 2t+1], per readiness chunk the time its list
- * wave passed the wait at [2 n_tiles + c], per list group its end at
- * [2 n_tiles + n_counters + g].  *words = total length (0 when tracing is off). */
+ * per tile [start, end, info] at [3t, 3t+1, 3t+2] (info = HW_ID | XCC_ID << 32
+ * | queue << 40 | slot << 44), per readiness chunk the time its list wave
+ * passed the wait at [3 n_tiles + c] and finished the chunk's blocks at
+ * [3 n_tiles + n_counters + n_groups + c], per list group its end at
+ * [3 n_tiles + n_counters + g].  *words = total length (0 when tracing is off). */
 int mirsha_pipeline_trace(mirsha_ctx* ctx, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words);
 int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t* n_counters, uint32_t* n_groups);
 /* Device-resident run: request digests to d_req_out (origin order), batch

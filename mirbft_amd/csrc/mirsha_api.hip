@@ -31,8 +31,10 @@ constexpr uint64_t kInlineArena = 1ull << 20;   // arenas up to this ride in the
 constexpr uint64_t kPinnedOutMax = 8ull << 20;  // digest results up to this come back via pinned staging
 
 constexpr uint64_t kArenaSlack = 256;           // loader may touch up to 80 B past a message
-constexpr uint32_t kFusedMaxListWaves = 64;      // chain waves of a fused launch (16 CUs)
+constexpr uint32_t kFusedMaxListWaves = 64;      // list groups (64 chains each) a fused launch takes
+constexpr uint32_t kFusedMaxListBlocks = 32;     // list CUs (one producer / consumer pair each)
 constexpr uint32_t kFusedMinChainBlocks = 64;    // AUTO picks the fused launch from this chain length
+constexpr uint32_t kFusedDefaultPace = 4;        // tile waves (= tile queues) per SIMD
 
 struct DevBuf {
     void* p = nullptr;
@@ -151,8 +153,8 @@ struct mirsha_pipeline {
     std::vector<uint32_t> tadj_first, tadj, cbase, expected;
     uint32_t n_tiles = 0, n_groups = 0, n_counters = 0, grid = 0;
     uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
-    uint32_t fused_flags = 0;                             // mirsha::kFusedTile* (MIRSHA_FUSED_FLAGS)
-    uint64_t tile_base = 0, list_base = 0;
+    uint64_t tile_base[mirsha::kFusedMaxQueues] = {};
+    uint32_t q_first[mirsha::kFusedMaxQueues + 1] = {};  // tile queues (fused_build)
     uint64_t epoch = 0;  // completed runs of a fused plan
     DevBuf d_tadj_first, d_tadj, d_cbase, d_expected, d_counters, d_ctl, d_trace;
     bool trace = false;
@@ -1038,23 +1040,28 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
         p->expected[(uint32_t)pairs[i]]++;
     }
     for (uint32_t t = 0; t < p->n_tiles; t++) p->tadj_first[t + 1] += p->tadj_first[t];
-    // Grid: one block per CU.  List blocks (4 chain waves each, alone on their
-    // SIMDs: a chain is latency-bound) + tile blocks on the remaining CUs with
-    // ONE tile wave per SIMD, so tiles complete in ticket order generation by
-    // generation and the chains can follow them (measured: two tile waves per
-    // SIMD halve the number of generations and lose, profiles/r01).
+    // Grid: one block per CU.  List blocks (one producer / consumer pair each
+    // on two SIMDs of an otherwise empty CU: a chain is latency-bound; group
+    // g on list block g mod list_blocks) + tile blocks on the remaining CUs with
+    // `pace` tile waves per SIMD, one per tile queue: queue q = the q-th run of
+    // W = 4 x tile_blocks tiles in needed-at order (the last queue takes the
+    // rest), served at issue priority 3 for queue 0 down to 0 for the last.
+    // MIRSHA_FUSED_PACE (1..4, A/B) overrides the default.
     hipDeviceProp_t prop;
     HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
     const uint32_t cus = (uint32_t)prop.multiProcessorCount;
-    p->pace = 1;
-    if (const char* e = getenv("MIRSHA_FUSED_PACE")) p->pace = std::min<uint32_t>(2u, std::max<uint32_t>(1u, (uint32_t)atoi(e)));
-    if (const char* e = getenv("MIRSHA_FUSED_FLAGS")) p->fused_flags = (uint32_t)atoi(e);
-    const uint32_t lw = std::min<uint32_t>(p->n_groups, kFusedMaxListWaves);
-    p->list_blocks = std::min<uint32_t>((lw + 3u) / 4u, cus / 4u);
+    p->pace = kFusedDefaultPace;
+    if (const char* e = getenv("MIRSHA_FUSED_PACE"))
+        p->pace = std::min<uint32_t>(mirsha::kPacedMaxPace, std::max<uint32_t>(1u, (uint32_t)atoi(e)));
+    // one list pair per group, up to kFusedMaxListBlocks CUs (more groups: each pair takes several)
+    p->list_blocks = std::min<uint32_t>(std::min<uint32_t>(p->n_groups, kFusedMaxListBlocks), cus / 8u);
     const uint32_t tile_blocks =
         std::max<uint32_t>(1, std::min<uint32_t>(cus - p->list_blocks, (p->n_tiles + 4u * p->pace - 1u) / (4u * p->pace)));
     p->tile_waves = tile_blocks * 4u * p->pace;
     p->grid = p->list_blocks + tile_blocks;
+    const uint32_t W = 4u * tile_blocks;  // tile waves per slot
+    for (uint32_t q = 0; q < p->pace; q++) p->q_first[q] = std::min<uint32_t>(p->n_tiles, q * W);
+    p->q_first[p->pace] = p->n_tiles;
     // Device copies.
     auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
         HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
@@ -1077,12 +1084,12 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     HIP_TRY(c, p->d_ctl.ensure(8ull * mirsha::kCtlWords));
     HIP_TRY(c, hipMemsetAsync(p->d_ctl.p, 0, 8ull * mirsha::kCtlWords, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    p->tile_base = p->list_base = 0;
+    for (uint64_t& b : p->tile_base) b = 0;
     p->epoch = 0;
     const char* tr = getenv("MIRSHA_FUSED_TRACE");
     p->trace = tr && atoi(tr) != 0;
     if (p->trace) {
-        const size_t words = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
+        const size_t words = 3ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
         HIP_TRY(c, p->d_trace.ensure(8ull * std::max<size_t>(words, 1)));
         HIP_TRY(c, hipMemsetAsync(p->d_trace.p, 0, 8ull * std::max<size_t>(words, 1), c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1110,8 +1117,10 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.ctl = p->d_ctl.as<unsigned long long>();
     a.trace = p->trace ? p->d_trace.as<unsigned long long>() : nullptr;
     a.n_counters = p->n_counters;
-    a.tile_base = p->tile_base;
-    a.list_base = p->list_base;
+    for (uint32_t q = 0; q < mirsha::kFusedMaxQueues; q++) a.tile_base[q] = p->tile_base[q];
+    for (uint32_t q = 0; q <= mirsha::kFusedMaxQueues; q++) a.q_first[q] = p->q_first[std::min(q, p->pace)];
+    a.n_queues = p->pace;
+    a.steal_own_prio = getenv_flag("MIRSHA_FUSED_STEAL_PRIO") ? 1u : 0u;
     a.arena_len = (uint32_t)arena_len;
     a.n_req = p->n_req;
     a.n_entries = p->n_entries;
@@ -1120,12 +1129,13 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.n_tiles = p->n_tiles;
     a.n_groups = p->n_groups;
     a.list_waves = p->list_blocks;
-    a.flags = p->fused_flags;
     if (int rc = timed_launch(c, 4, [&] { return mirsha::launch_fused_paced(a, p->grid, p->pace, c->stream); }))
         return rc;
-    // Tile waves and list waves each made exactly one failing claim on their ticket.
-    p->tile_base += p->n_tiles + p->tile_waves;
-    p->list_base += p->n_groups + (uint64_t)p->list_blocks * 4u;
+    // Every tile wave made exactly one failing claim on its own queue and one on
+    // the last queue (the same one for the last slot).
+    const uint32_t last = p->pace - 1u, W = p->tile_waves / p->pace;
+    for (uint32_t q = 0; q < p->pace; q++)
+        p->tile_base[q] += (p->q_first[q + 1] - p->q_first[q]) + (q == last ? p->tile_waves : W);
     p->epoch++;
     return MIRSHA_OK;
 }
@@ -1704,7 +1714,7 @@ int mirsha_pipeline_trace(mirsha_ctx* c, mirsha_pipeline* p, uint64_t* out, uint
     if (p->mode != MIRSHA_PIPELINE_FUSED || !p->trace) return MIRSHA_OK;
     if (int rc = use_device(c)) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    const uint64_t n = 2ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
+    const uint64_t n = 3ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
     *words = n;
     if (out && cap) {
         HIP_TRY(c, hipMemcpyAsync(out, p->d_trace.p, 8ull * std::min(n, cap), hipMemcpyDeviceToHost, c->stream));

@@ -62,8 +62,13 @@ hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32
 hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                              const uint32_t* cfirst, uint32_t n_lists, uint8_t* out, hipStream_t s);
 // Fused request -> list pass (one persistent launch), see mirsha_kernels.hip.
-constexpr uint32_t kFusedChunkBlocks = 4;  // list blocks (8 digests) per readiness chunk
-constexpr uint32_t kCtlTileTicket = 0, kCtlListTicket = 16, kCtlError = 32, kCtlWords = 48;  // u64 words
+constexpr uint32_t kFusedChunkBlocks = 2;  // list blocks (4 digests) per readiness chunk
+// Tile queues of the fused launch: queue q holds tiles [q_first[q], q_first[q+1])
+// in needed-at order and is served first by the tile waves of slot q on every
+// SIMD, at issue priority prio_of(q) (earliest-needed tiles win issue).
+constexpr uint32_t kFusedMaxQueues = 4;
+// ctl words (u64): tile tickets at kCtlTileTicket + 16 q, error flag (one 128-B line each)
+constexpr uint32_t kCtlTileTicket = 0, kCtlError = 64, kCtlWords = 80;
 struct FusedArgs {
     const uint8_t* arena;
     const uint64_t* off;
@@ -79,24 +84,28 @@ struct FusedArgs {
     const uint32_t* expected;    // tiles feeding each counter
     unsigned long long* counters;
     unsigned long long* ctl;     // kCtlWords: tickets + error flag, one 128-B line each
-    // Optional timeline (s_memrealtime, 100 MHz), NULL = off: per tile [start, end]
-    // at [2t, 2t+1]; per readiness chunk the time its list wave passed the wait
-    // at [2 n_tiles + ctr]; per list group its end at [2 n_tiles + n_counters + g].
+    // Optional timeline (s_memrealtime, 100 MHz), NULL = off: per tile [start, end,
+    // info] at [3t, 3t+1, 3t+2] (info = HW_ID | XCC_ID << 32 | queue << 40 | slot << 44);
+    // per readiness chunk the time its list wave passed the wait at
+    // [3 n_tiles + ctr] and finished its blocks at [3 n_tiles + n_counters +
+    // n_groups + ctr]; per list group its end at [3 n_tiles + n_counters + g].
     unsigned long long* trace;
     uint32_t n_counters;
-    unsigned long long tile_base, list_base;
+    unsigned long long tile_base[kFusedMaxQueues];
+    uint32_t q_first[kFusedMaxQueues + 1];
+    uint32_t n_queues;  // = tile waves per SIMD (pace)
+    uint32_t steal_own_prio;  // A/B (MIRSHA_FUSED_STEAL_PRIO=1): tiles taken from the last queue keep the taker's priority
     uint32_t arena_len, n_req, n_entries, n_lists;
     // Run number of the plan (1, 2, ...): counters are monotone over runs and a
     // chunk is ready at epoch x expected; 64-bit so it never wraps.
     unsigned long long epoch;
     uint32_t n_tiles, n_groups, list_waves;
-    uint32_t flags;  // kFusedTilePrio | kFusedTileYield (A/B knobs, MIRSHA_FUSED_FLAGS)
 };
-constexpr uint32_t kFusedTilePrio = 1;   // s_setprio 2/1/0 for tiles by ticket third (early tiles first)
-constexpr uint32_t kFusedTileYield = 2;  // issue-yield rounds in tile waves (pace >= 2)
 // list_waves = number of list BLOCKS (first in the grid); one block per CU
-// (kPacedLds of reserved LDS), `pace` tile waves per SIMD in tile blocks.
+// (kPacedLds of LDS: the tile waves' 4 KiB staging tiles, and enough to keep
+// any second block off the CU), `pace` tile waves per SIMD in tile blocks.
 constexpr uint32_t kPacedLds = 96u * 1024u;
+constexpr uint32_t kPacedMaxPace = 4;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.

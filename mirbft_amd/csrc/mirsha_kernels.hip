@@ -272,11 +272,28 @@ __device__ __forceinline__ void progress_prio(uint32_t blk) {
 // [64 t, 64 t + 64) (order[] maps a position to a message; NULL = identity).
 // kLds: LDS-staged coalesced loader (else direct per-lane loads); kWide:
 // 64-bit per-lane addresses for arenas beyond one buffer descriptor.
-template <bool kLds, bool kWide>
+// Fixed issue priority of a fused-launch tile wave (its queue's), set before
+// each block's rounds in place of progress_prio.
+__device__ __forceinline__ void fixed_prio(uint32_t p) {
+    if (p >= 3u) __builtin_amdgcn_s_setprio(3);
+    else if (p == 2u) __builtin_amdgcn_s_setprio(2);
+    else if (p == 1u) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
+
+// kFused (sha256_fused_paced_kernel's tile waves): blocks at the fixed
+// priority fprio, digests stored with sc1 for list waves on other CUs.
+template <bool kLds, bool kWide, bool kFused = false>
 __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
-                                          uint4* my, uint32_t t, uint32_t lane) {
+                                          uint4* my, uint32_t t, uint32_t lane, uint32_t fprio = 0) {
+    auto block_prio = [&](uint32_t blk) {
+        if constexpr (kFused)
+            fixed_prio(fprio);
+        else
+            progress_prio(blk);
+    };
     // Prologue at the highest issue priority, back to 0 at the first
     // compression: a fresh wave is the youngest on its SIMD and at the default
     // priority gets the VALU only when every older wave stalls, so its
@@ -490,7 +507,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                 asm volatile("s_mov_b32 %0, %1" : "=s"(wnb) : "s"(wave_nb));
                 pad_block_uniform(w, soff, min_l, wnb - blk == 1u);
             }
-            progress_prio(blk);
+            block_prio(blk);
             if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm(st, w);
         }
@@ -509,7 +526,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
             stage(blk, w, ln, true);
             pad_block_uniform<4>(w, 64u * blk, min_l, false);
-            progress_prio(blk);
+            block_prio(blk);
             if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm_tail(st, w, tw);
         }
@@ -568,7 +585,11 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         }
     }
     if (valid) {
-        if constexpr (kLds && !kWide) {
+        if constexpr (kFused) {
+            const __amdgpu_buffer_rsrc_t ors =
+                __builtin_amdgcn_make_buffer_rsrc((void*)out, (short)0, (int)(32u * n), 0x00020000);
+            store_digest_sc1(ors, msg, st);
+        } else if constexpr (kLds && !kWide) {
             // 32-bit buffer offsets (launch_msgs sends n >= 2^27 to the wide
             // form): the message index stays one VGPR across the block loop
             // instead of a 64-bit address pair (the tail form spilled it).
@@ -1119,74 +1140,128 @@ __device__ __forceinline__ void load_digest_sc1(__amdgpu_buffer_rsrc_t rsrc, uin
 }
 
 // Chain form of a list group for the paced kernel: a lane's list is consumed
-// a whole readiness chunk (kFusedChunkBlocks blocks = 8 digests) at a time,
-// double-buffered in registers, so one chunk's digest loads (sc1, served from
-// MALL/HBM under full request load: several us) are in flight while the
-// previous chunk is compressed.  Indices are static and loaded a chunk ahead.
+// a whole readiness chunk (kFusedChunkBlocks blocks = kChunkDigests digests) at
+// a time, double-buffered in registers, so one chunk's digest loads (sc1,
+// served from MALL/HBM under full request load: several us) are in flight
+// while the previous chunk is compressed.  Indices are static and loaded a
+// chunk ahead.  (2-block chunks: the launch's 1024-thread tile blocks hold the
+// kernel to 128 VGPRs.)
+constexpr uint32_t kChunkDigests = 2u * kFusedChunkBlocks;
 __device__ __forceinline__ void load_chunk_idx(__amdgpu_buffer_rsrc_t irs, uint32_t e0, uint32_t c, uint32_t chunk,
-                                               uint32_t ix[8]) {
+                                               uint32_t ix[kChunkDigests]) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint32_t o = 8u * chunk + (uint32_t)i;
+    for (uint32_t i = 0; i < kChunkDigests; i++) {
+        const uint32_t o = kChunkDigests * chunk + i;
         ix[i] = ld_u32(irs, 4u * (e0 + o), o < c);
     }
 }
 
-__device__ __forceinline__ void load_chunk_digests(__amdgpu_buffer_rsrc_t drs, const uint32_t ix[8], uint32_t c,
-                                                   uint32_t chunk, bool go, uint4 d[16]) {
+__device__ __forceinline__ void load_chunk_digests(__amdgpu_buffer_rsrc_t drs, const uint32_t ix[kChunkDigests],
+                                                   uint32_t c, uint32_t chunk, bool go, uint4 d[2 * kChunkDigests]) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) load_digest_sc1(drs, ix[i], go && 8u * chunk + (uint32_t)i < c, d[2 * i], d[2 * i + 1]);
+    for (uint32_t i = 0; i < kChunkDigests; i++)
+        load_digest_sc1(drs, ix[i], go && kChunkDigests * chunk + i < c, d[2 * i], d[2 * i + 1]);
 }
 
-__device__ __forceinline__ void fused_list_group_deep(const FusedArgs& a, __amdgpu_buffer_rsrc_t drs,
-                                                      __amdgpu_buffer_rsrc_t irs, uint32_t g, uint32_t lane) {
-    static_assert(kFusedChunkBlocks == 4, "chunk = 4 blocks = 8 digests");
-    const uint32_t k = g * 64u + lane;
-    const bool valid = k < a.n_lists;
-    const uint32_t e0 = valid ? a.cfirst[k] : 0u;
-    const uint32_t c = valid ? a.cfirst[k + 1] - e0 : 0u;
-    const uint32_t L = 32u * c;
-    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
-    const uint32_t wave_nb = wave_max(nb);
-    const uint32_t nchunks = (wave_nb + 3u) / 4u;
+// Producer/consumer hand-off of a fused list pair (one per list block, two
+// waves on two SIMDs): the producer builds each block's words from the list's
+// digests (readiness waits, sc1 loads), computes the schedule and K + W into
+// ring slot seq & 1 and publishes seq + 1; the consumer runs the rounds from
+// that slot and frees it.  LDS flags with workgroup-scope acquire / release
+// (no s_barrier: the list block's other waves have exited); the waits carry
+// the same 2 s watchdog as the readiness waits.
+struct FusedPairRing {
+    uint4 kw[2][16][64];
+    uint32_t produced, consumed;  // blocks handed over / freed, over all groups of the block
+};
+
+__device__ __forceinline__ bool lds_wait_ge(const uint32_t* p, uint32_t target, unsigned long long* err) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
+            __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ void lds_publish(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Shape of list group g for this lane's list.
+struct FusedListShape {
+    uint32_t k, e0, c, L, nb, wave_nb;
+    bool valid;
+    __device__ FusedListShape(const FusedArgs& a, uint32_t g, uint32_t lane) {
+        k = g * 64u + lane;
+        valid = k < a.n_lists;
+        e0 = valid ? a.cfirst[k] : 0u;
+        c = valid ? a.cfirst[k + 1] - e0 : 0u;
+        L = 32u * c;
+        nb = valid ? blocks_for_len(L) : 0u;
+        wave_nb = wave_max(nb);
+    }
+};
+
+// Consumer side of group g: the rounds of every block from the ring.
+__device__ __forceinline__ void fused_list_consume(const FusedArgs& a, FusedPairRing& ring, uint32_t g,
+                                                   uint32_t lane, uint32_t& seq) {
+    const FusedListShape sh(a, g, lane);
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    for (uint32_t blk = 0; blk < sh.wave_nb; blk++, seq++) {
+        if (!lds_wait_ge(&ring.produced, seq + 1u, a.ctl + kCtlError)) return;
+        consume_kw(ring.kw[seq & 1u], lane, st, blk < sh.nb);
+        lds_publish(&ring.consumed, seq + 1u);
+    }
+    if (a.trace && lane == 0) a.trace[3u * a.n_tiles + a.n_counters + g] = __builtin_amdgcn_s_memrealtime();
+    if (sh.valid) store_digest(a.list_out, sh.k, st);
+}
+
+// Producer side of group g: readiness waits and digest loads a chunk ahead,
+// then each block's schedule + K + W into the ring.
+__device__ __forceinline__ void fused_list_produce(const FusedArgs& a, __amdgpu_buffer_rsrc_t drs,
+                                                   __amdgpu_buffer_rsrc_t irs, FusedPairRing& ring, uint32_t g,
+                                                   uint32_t lane, uint32_t& seq) {
+    const FusedListShape sh(a, g, lane);
+    const uint32_t e0 = sh.e0, c = sh.c, L = sh.L, wave_nb = sh.wave_nb;
+    const uint32_t nchunks = (wave_nb + kFusedChunkBlocks - 1u) / kFusedChunkBlocks;
     const uint32_t cb = a.cbase[g];
     auto target = [&](uint32_t chunk) -> uint64_t { return (uint64_t)a.epoch * a.expected[cb + chunk]; };
     auto stamp = [&](uint32_t at) {
         if (a.trace && lane == 0) a.trace[at] = __builtin_amdgcn_s_memrealtime();
     };
-    uint32_t st[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) st[i] = kH0[i];
-    if (nchunks == 0) {
-        stamp(2u * a.n_tiles + a.n_counters + g);
-        return;
-    }
-    uint32_t ixc[8], ixn[8];
+    if (nchunks == 0) return;
+    uint32_t ixc[kChunkDigests], ixn[kChunkDigests];
     load_chunk_idx(irs, e0, c, 0u, ixc);
     load_chunk_idx(irs, e0, c, 1u, ixn);
     wait_counter(a.counters + cb, target(0), a.ctl + kCtlError);
-    uint4 dc[16];
+    uint4 dc[2 * kChunkDigests];
     load_chunk_digests(drs, ixc, c, 0u, true, dc);
     uint64_t pollv = 1u < nchunks ? poll_counter(a.counters + cb + 1u) : 0u;
     for (uint32_t chunk = 0; chunk < nchunks; chunk++) {
-        stamp(2u * a.n_tiles + cb + chunk);
+        stamp(3u * a.n_tiles + cb + chunk);
         // Next chunk's digests now if its tiles are done (poll issued one chunk ago).
         const uint32_t nc = chunk + 1u;
         bool have_next = false;
-        uint4 dn[16];
+        uint4 dn[2 * kChunkDigests];
         if (nc < nchunks) {
             have_next = (bool)__shfl((int)(pollv >= target(nc)), 0, 64);
             load_chunk_digests(drs, ixn, c, nc, have_next, dn);
         }
-        uint32_t ixnn[8];
+        uint32_t ixnn[kChunkDigests];
         load_chunk_idx(irs, e0, c, chunk + 2u, ixnn);
         if (!have_next && nc + 1u < nchunks) pollv = 0;
         if (have_next && nc + 1u < nchunks) pollv = poll_counter(a.counters + cb + nc + 1u);
         else if (nc < nchunks) pollv = poll_counter(a.counters + cb + nc);
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t blk = 4u * chunk + (uint32_t)j;
-            if (blk < nb) {
+        for (uint32_t j = 0; j < kFusedChunkBlocks; j++) {
+            const uint32_t blk = kFusedChunkBlocks * chunk + j;
+            if (blk < wave_nb) {  // wave-uniform: dead lanes hand over words the consumer ignores
                 uint32_t w[16];
 #pragma unroll
                 for (int half = 0; half < 2; half++) {
@@ -1198,14 +1273,18 @@ __device__ __forceinline__ void fused_list_group_deep(const FusedArgs& a, __amdg
                     w[8 * half + 5] = __builtin_bswap32(x1.y); w[8 * half + 6] = __builtin_bswap32(x1.z);
                     w[8 * half + 7] = __builtin_bswap32(x1.w);
                 }
-                if (blk + 1u == nb) {
+                if (blk + 1u == sh.nb) {
                     w[14] = L >> 29;
                     w[15] = L << 3;
                 }
-                compress_asm_lat(st, w);
+                // slot seq & 1 was last filled with block seq - 2: free once seq - 1 blocks are consumed
+                if (seq >= 2u && !lds_wait_ge(&ring.consumed, seq - 1u, a.ctl + kCtlError)) return;
+                produce_kw(w, ring.kw[seq & 1u], lane);
+                lds_publish(&ring.produced, seq + 1u);
+                seq++;
             }
         }
-        stamp(2u * a.n_tiles + a.n_counters + a.n_groups + cb + chunk);
+        stamp(3u * a.n_tiles + a.n_counters + a.n_groups + cb + chunk);
         if (nc < nchunks) {
             if (!have_next) {  // exposed: wait for the next chunk's tiles, then load it
                 wait_counter(a.counters + cb + nc, target(nc), a.ctl + kCtlError);
@@ -1213,104 +1292,89 @@ __device__ __forceinline__ void fused_list_group_deep(const FusedArgs& a, __amdg
                 if (nc + 1u < nchunks) pollv = poll_counter(a.counters + cb + nc + 1u);
             }
 #pragma unroll
-            for (int i = 0; i < 16; i++) dc[i] = dn[i];
+            for (uint32_t i = 0; i < 2 * kChunkDigests; i++) dc[i] = dn[i];
 #pragma unroll
-            for (int i = 0; i < 8; i++) ixn[i] = ixnn[i];
+            for (uint32_t i = 0; i < kChunkDigests; i++) ixn[i] = ixnn[i];
         }
     }
-    stamp(2u * a.n_tiles + a.n_counters + g);
-    if (valid) store_digest(a.list_out, k, st);
 }
 
-// Tile loader prefetching kTileDepth blocks ahead (paced kernel: a tile wave is
-// alone on its SIMD, and a load under full request load takes several us).
-constexpr int kTileDepth = 3;
-template <bool kYield>
-__device__ __forceinline__ void hash_tile_deep(const uint8_t* __restrict__ arena, uint32_t arena_len,
-                                               const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
-                                               const uint32_t* __restrict__ order, uint32_t n,
-                                               __amdgpu_buffer_rsrc_t ors, uint32_t t, uint32_t lane) {
-    const uint32_t slot = t * 64u + lane;
-    const bool valid = slot < n;
-    const uint32_t msg = valid ? order[slot] : 0u;
-    const uint32_t L = valid ? len[msg] : 0u;
-    const uint32_t o = valid ? (uint32_t)off[msg] : 0u;
-    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
-    const uint32_t wave_nb = wave_max(nb);
-    const uint32_t records = (arena_len + 3u) & ~3u;
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)arena, (short)0, (int)records, 0x00020000);
-    uint32_t st[8];
-#pragma unroll
-    for (int i = 0; i < 8; i++) st[i] = kH0[i];
-    RawChunk rc[kTileDepth][4];
-#pragma unroll
-    for (int d = 0; d < kTileDepth; d++)
-#pragma unroll
-        for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, (uint32_t)d, (uint32_t)q, (uint32_t)d < nb, rc[d][q]);
-    for (uint32_t blk = 0; blk < wave_nb; blk++) {
-        uint32_t w[16];
-#pragma unroll
-        for (int q = 0; q < 4; q++) finish_chunk(rc[0][q], 64u * blk + 16u * q, L, blk + 1u == nb, (uint32_t)q, &w[4 * q]);
-#pragma unroll
-        for (int d = 0; d + 1 < kTileDepth; d++)
-#pragma unroll
-            for (int q = 0; q < 4; q++) rc[d][q] = rc[d + 1][q];
-        const uint32_t nbk = blk + (uint32_t)kTileDepth;
-#pragma unroll
-        for (int q = 0; q < 4; q++) issue_chunk(rsrc, records, o, nbk, (uint32_t)q, nbk < nb, rc[kTileDepth - 1][q]);
-        if (blk < nb) {
-            if constexpr (kYield)
-                compress_asm(st, w);
-            else
-                compress_asm_lat(st, w);
-        }
-    }
-    if (valid) store_digest_sc1(ors, msg, st);
+// Block = 4 x pace waves (pace per SIMD; wave w on SIMD w % 4), one block per
+// CU (kPacedLds of LDS).  List blocks [0, list_blocks) run one chain wave per
+// SIMD ALONE on their CU (waves 4.. of a list block exit at once).  Tile
+// blocks fill the other CUs with `pace` tile waves per SIMD, one per tile
+// QUEUE: the wave of slot q = w / 4 serves queue q (tiles in needed-at order,
+// queue 0 the earliest) at issue priority prio_of(q), so on every SIMD the
+// wave holding the earliest-needed tile wins issue and finishes first while
+// the later queues soak up the remaining issue slots (the SIMD stays full, the
+// chains get their digests in needed-at order); a wave whose queue is empty
+// takes tiles from the last queue.  The tile waves run the request kernel's
+// LDS-staged, yield-form hash_tile.
+constexpr uint32_t kPacedMaxThreads = 256u * kPacedMaxPace;
+__device__ __forceinline__ uint32_t prio_of(uint32_t q, uint32_t nq) {
+    return q == 0u ? 3u : nq - 1u - q;  // 4 queues: 3 2 1 0; 2 queues: 3 0
 }
 
-// Block = 4 x pace waves (pace per SIMD), one block per CU (the launch asks
-// for kPacedLds bytes of LDS it never touches, which keeps any second block
-// off the CU): list blocks [0, list_blocks) run one chain wave per SIMD ALONE
-// on their CU (waves 4.. of a list block exit at once); tile blocks fill the
-// other CUs with `pace` tile waves per SIMD.
-constexpr uint32_t kPacedMaxThreads = 512;
 __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(FusedArgs a) {
+    extern __shared__ uint4 paced_lds[];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
     const __amdgpu_buffer_rsrc_t drs =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.req_out, (short)0, (int)(32u * a.n_req), 0x00020000);
-    if (blockIdx.x < a.list_waves) {  // list_waves carries the number of LIST BLOCKS here
-        if (wv >= 4u) return;
+    // Slot = this wave's rank among the block's waves on its SIMD (HW_ID), so
+    // every SIMD hosts one tile wave per queue, and a list pair spans two
+    // SIMDs, whatever the dispatcher's wave placement.
+    __shared__ uint32_t simd_waves[4];
+    FusedPairRing& ring = *reinterpret_cast<FusedPairRing*>(paced_lds);
+    const bool list_block = blockIdx.x < a.list_waves;  // list_waves carries the number of LIST BLOCKS
+    if (threadIdx.x < 4u) simd_waves[threadIdx.x] = 0u;
+    if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = 0u;
+    __syncthreads();
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const uint32_t simd = (hw >> 4) & 3u;
+    uint32_t slot = 0u;
+    if (lane == 0u) slot = atomicAdd(&simd_waves[simd], 1u);
+    slot = (uint32_t)__shfl((int)slot, 0, 64);
+    if (list_block) {  // groups blockIdx.x, + list blocks, ...: producer on SIMD 0, consumer on SIMD 1
+        if (slot != 0u || simd > 1u) return;
         __builtin_amdgcn_s_setprio(3);
-        const __amdgpu_buffer_rsrc_t irs =
-            __builtin_amdgcn_make_buffer_rsrc((void*)a.cidx, (short)0, (int)(4u * a.n_entries), 0x00020000);
-        while (true) {
-            const uint64_t g = claim(a.ctl + kCtlListTicket, lane) - a.list_base;
-            if (g >= a.n_groups) break;
-            fused_list_group_deep(a, drs, irs, (uint32_t)g, lane);
+        uint32_t seq = 0u;
+        if (simd == 0u) {
+            const __amdgpu_buffer_rsrc_t irs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)a.cidx, (short)0, (int)(4u * a.n_entries), 0x00020000);
+            for (uint32_t g = blockIdx.x; g < a.n_groups; g += a.list_waves)
+                fused_list_produce(a, drs, irs, ring, g, lane, seq);
+        } else {
+            for (uint32_t g = blockIdx.x; g < a.n_groups; g += a.list_waves) fused_list_consume(a, ring, g, lane, seq);
         }
         return;
     }
+    uint4* my = paced_lds + 256u * wv;  // the wave's 4 KiB staging tile
+    const uint32_t last = a.n_queues - 1u;
+    const uint32_t q = min(slot, last);
+    bool own = true;
     while (true) {
-        const uint64_t t = claim(a.ctl + kCtlTileTicket, lane) - a.tile_base;
-        if (t >= a.n_tiles) break;
-        if (a.trace && lane == 0) a.trace[2 * t] = __builtin_amdgcn_s_memrealtime();
-        if (a.flags & kFusedTilePrio) {  // early tickets feed the chains first: let them win issue
-            const uint32_t third = (uint32_t)((3ull * t) / a.n_tiles);
-            if (third == 0)
-                __builtin_amdgcn_s_setprio(2);
-            else if (third == 1)
-                __builtin_amdgcn_s_setprio(1);
-            else
-                __builtin_amdgcn_s_setprio(0);
+        const uint32_t qq = own ? q : last;
+        const uint64_t t = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) - a.tile_base[qq] + a.q_first[qq];
+        if (t >= a.q_first[qq + 1]) {
+            if (own && qq != last) {
+                own = false;
+                continue;
+            }
+            break;
         }
-        if (a.flags & kFusedTileYield)
-            hash_tile_deep<true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, drs, (uint32_t)t, lane);
-        else
-            hash_tile_deep<false>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, drs, (uint32_t)t, lane);
+        if (a.trace && lane == 0) {
+            uint32_t xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            a.trace[3 * t] = __builtin_amdgcn_s_memrealtime();
+            a.trace[3 * t + 2] = (unsigned long long)hw | ((unsigned long long)(xcc & 0xFFu) << 32) |
+                                 ((unsigned long long)qq << 40) | ((unsigned long long)slot << 44);
+        }
+        hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, a.req_out, my,
+                                     (uint32_t)t, lane, prio_of(a.steal_own_prio ? q : qq, a.n_queues));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.trace && lane == 0) a.trace[2 * t + 1] = __builtin_amdgcn_s_memrealtime();
+        if (a.trace && lane == 0) a.trace[3 * t + 1] = __builtin_amdgcn_s_memrealtime();
         const uint32_t j0 = a.tadj_first[t], j1 = a.tadj_first[t + 1];
         for (uint32_t j = j0 + lane; j < j1; j += 64u)
             __hip_atomic_fetch_add(a.counters + a.tadj[j], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1493,7 +1557,7 @@ hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const u
 
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s) {
     if (grid == 0) return hipSuccess;
-    if (pace < 1 || 64u * 4u * pace > kPacedMaxThreads) return hipErrorInvalidValue;
+    if (pace < 1 || pace > kPacedMaxPace || a.n_queues != pace) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)sha256_fused_paced_kernel,

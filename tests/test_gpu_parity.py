@@ -505,8 +505,11 @@ def test_pipeline_irregular_lists(engine, monkeypatch, env_mode):
     (34, 1, 3, 40, 10),              # one request, repeated in every list
     (35, 5000, 2, 0, 2000),          # only empty lists (no entries): padding block only
 ])
-def test_fused_plan_irregular(engine, seed, n, n_lists, max_list, max_len):
-    """Fused plan (device API) on irregular shapes, three runs on one plan."""
+@pytest.mark.parametrize("pace", [1, 2, 4])
+def test_fused_plan_irregular(engine, monkeypatch, pace, seed, n, n_lists, max_list, max_len):
+    """Fused plan (device API) on irregular shapes, three runs on one plan (the
+    tile queues' tickets carried across runs), 1, 2 or 4 tile queues."""
+    monkeypatch.setenv("MIRSHA_FUSED_PACE", str(pace))
     arena, off, lens, idx, first = _irregular(seed, n, n_lists, max(max_list, 1), max_len)
     if max_list == 0:
         first = np.zeros(n_lists + 1, dtype=np.uint32)
@@ -520,11 +523,14 @@ def test_fused_plan_irregular(engine, seed, n, n_lists, max_list, max_len):
     plan.close()
 
 
-def test_fused_plans_interleaved(engine):
-    """Two fused plans used alternately: each keeps its own tickets / counters."""
+def test_fused_plans_interleaved(engine, monkeypatch):
+    """Two fused plans used alternately: each keeps its own tickets / counters
+    (3 and 4 tile queues)."""
     a = _irregular(41, 2000, 200, 40, 400)
     b = _irregular(42, 5000, 90, 300, 200)
+    monkeypatch.setenv("MIRSHA_FUSED_PACE", "3")
     pa = engine.pipeline(a[2].size, a[3], a[4], a[2], mode="fused")
+    monkeypatch.setenv("MIRSHA_FUSED_PACE", "4")
     pb = engine.pipeline(b[2].size, b[3], b[4], b[2], mode="fused")
     for _ in range(2):
         for (arena, off, lens, idx, first), plan in ((a, pa), (b, pb)):

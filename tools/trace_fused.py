@@ -43,15 +43,25 @@ def main():
         plan.status()
         tr = plan.trace().astype(np.int64)
         nt, nc, ng = plan.shape()
-        ts, te = tr[0:2 * nt:2], tr[1:2 * nt:2]
-        chunk = tr[2 * nt:2 * nt + nc]
-        gend = tr[2 * nt + nc:2 * nt + nc + ng]
-        cend = tr[2 * nt + nc + ng:2 * nt + 2 * nc + ng]
+        ts, te, info = tr[0:3 * nt:3], tr[1:3 * nt:3], tr[2:3 * nt:3]
+        chunk = tr[3 * nt:3 * nt + nc]
+        gend = tr[3 * nt + nc:3 * nt + nc + ng]
+        cend = tr[3 * nt + nc + ng:3 * nt + 2 * nc + ng]
+        queue, slot = (info >> 40) & 0xF, (info >> 44) & 0xF
+        simd_key = ((info >> 32) & 0xFF) << 16 | ((info & 0xFFFFFFFF) >> 4) & 0xFFF
         t0 = ts.min()
         us = lambda x: (x - t0) / 100.0  # noqa: E731  (100 MHz ticks -> us)
         dur = (te - ts) / 100.0
         q = lambda a: [round(float(np.percentile(a, p)), 1) for p in (0, 10, 50, 90, 100)]  # noqa: E731
-        res = {"config": cfg, "pace": pace, "tiles": nt, "counters": nc, "groups": ng,
+        per_q = {}
+        for qq in np.unique(queue):
+            m = queue == qq
+            per_q[int(qq)] = {"tiles": int(m.sum()), "end_us_pcts": q(us(te[m])), "dur_us_pcts": q(dur[m]),
+                              "start_us_pcts": q(us(ts[m]))}
+        # waves of one SIMD per queue (the slot assignment puts one of each queue on every SIMD)
+        _, per_simd = np.unique(simd_key, return_counts=True)
+        res = {"config": cfg, "pace": pace, "tiles": nt, "counters": nc, "groups": ng, "per_queue": per_q,
+               "tiles_per_simd_pcts": q(per_simd),
                "tile_start_us_pcts": q(us(ts)), "tile_end_us_pcts": q(us(te)), "tile_dur_us_pcts": q(dur),
                "group_end_us": q(us(gend)), "kernel_span_us": round(float(us(max(te.max(), gend.max()))), 1)}
         # group 0's chunks: pass time vs when the tiles it needs ended (needed-at order rebuilt here)
