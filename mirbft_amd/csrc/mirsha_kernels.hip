@@ -29,13 +29,16 @@ namespace mirsha {
 // the four row results by v_readlane and a scalar reduction.  Called with all
 // 64 lanes active (every call site is at a kernel's top, before divergence);
 // a DPP source outside the row keeps the lane's own value.
+// (The DPP moves' "old" operand is the op's identity, so hipcc folds each
+// move into the max / min itself: v_max_u32_dpp, one VALU per step.)
 template <bool kMax>
 __device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
     auto op = [](uint32_t a, uint32_t b) { return kMax ? (a > b ? a : b) : (a < b ? a : b); };
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
-    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
+    constexpr int id = kMax ? 0 : -1;
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x124, 0xF, 0xF, false));  // row_ror:4
+    v = op(v, (uint32_t)__builtin_amdgcn_update_dpp(id, (int)v, 0x128, 0xF, 0xF, false));  // row_ror:8
     const uint32_t r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
     const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
     return op(op(r0, r1), op(r2, r3));
@@ -326,7 +329,10 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     const uint64_t o = valid ? o_ : 0u;
 #endif
     const uint32_t nb = valid ? blocks_for_len(L) : 0u;
-    const uint32_t wave_nb = wave_max(nb);  // wave-uniform (SGPR): scalar block-loop tests
+    // The tile's longest message, and from it (blocks_for_len is monotone) the
+    // wave-uniform block count (SGPR: scalar block-loop tests).
+    const uint32_t max_l = wave_max(valid ? L : 0u);
+    const uint32_t wave_nb = blocks_for_len(max_l);
 
     // Bytes past arena_len inside the last dword are never part of a message
     // (they are masked by the padding logic), so the range rounds up to 4.
@@ -378,7 +384,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 #ifdef MIRSHA_AB_PRODUCER_PAD  // A/B build only: loader-side padding for every tile
         const bool uni = false;
 #else
-        const bool uni = wave_max(valid ? L : 0u) == min_l;
+        const bool uni = max_l == min_l;
 #endif
         // Final-block tail form (compress_asm_tail) for uniform tiles whose
         // final block holds at most 16 message bytes; its scalars up front.
