@@ -8,7 +8,7 @@
 #include <stdint.h>
 
 #include "sha256_rounds_asm.h"
-#if defined(MIRSHA_AB_KSGPR) || defined(MIRSHA_AB_ROUNDS)  // A/B builds only (tools/ab_build.sh)
+#if defined(MIRSHA_AB_KSGPR) || defined(MIRSHA_AB_ROUNDS) || defined(MIRSHA_AB_LAT_ROUNDS)  // A/B builds only (tools/ab_build.sh)
 #include "sha256_rounds_asm_ab.h"
 #endif
 
@@ -136,7 +136,11 @@ __device__ __forceinline__ void compress_asm_lat(uint32_t st[8], uint32_t w[16])
     uint32_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = st[i];
+#if defined(MIRSHA_AB_LAT_ROUNDS)  // e.g. -DMIRSHA_AB_LAT_ROUNDS=rounds_asm_ilp
+    MIRSHA_AB_LAT_ROUNDS(s, w);
+#else
     rounds_asm_nonop(s, w);
+#endif
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] += s[i];
 }

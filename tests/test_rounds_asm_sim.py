@@ -102,8 +102,11 @@ def run_asm(lines, regs):
 
 
 # ---- header parsing ----------------------------------------------------------
-def _functions():
-    text = open(HDR).read()
+AB_HDR = os.path.join(ROOT, "tools", "sha256_rounds_asm_ab.h")
+
+
+def _functions(path=HDR):
+    text = open(path).read()
     fns = {}
     for m in re.finditer(r"__device__ __forceinline__ void (\w+)\(([^)]*)\) \{(.*?)\n\}\n", text, re.S):
         fns[m.group(1)] = (m.group(2), m.group(3))
@@ -125,10 +128,10 @@ def _statements(body):
     return out
 
 
-def run_function(name, env):
+def run_function(name, env, path=HDR):
     """Run generated function `name`; env maps C expressions (s[0], w[3], k.c4,
     k0.x ...) to values and is updated for the "+" / "=" operands."""
-    _, body = _functions()[name]
+    _, body = _functions(path)[name]
     for lines, operands in _statements(body):
         regs = {}
         for i, (nm, expr, cons) in enumerate(operands):
@@ -194,3 +197,18 @@ def test_rounds_kw8_asm_matches_fips():
         env.update({f"k1.{x}": kw[4 + i] for i, x in enumerate("xyzw")})
         run_function("rounds_kw8_asm", env)
     assert [env[f"s[{i}]"] for i in range(8)] == ref_rounds(s, w)
+
+
+def test_ab_round_forms_match_fips():
+    """The A/B-only forms (tools/sha256_rounds_asm_ab.h: yield patterns,
+    K-in-SGPR, bfi / add2 / literal variants, the lone-wave ILP order) are
+    bit-identical to FIPS 180-4 too."""
+    rng = random.Random(4)
+    names = [n for n, (sig, _) in _functions(AB_HDR).items() if "uint32_t w[16]" in sig]
+    assert "rounds_asm_ilp" in names and len(names) >= 8
+    for name in names:
+        s, w = _rand_state(rng), [rng.getrandbits(32) for _ in range(16)]
+        env = {f"s[{i}]": s[i] for i in range(8)}
+        env.update({f"w[{i}]": w[i] for i in range(16)})
+        run_function(name, env, AB_HDR)
+        assert [env[f"s[{i}]"] for i in range(8)] == ref_rounds(s, w), name

@@ -14,6 +14,7 @@
 #   spawn:     -DMIRSHA_AB_SPAWN_THREADS (host passes on threads spawned per call instead of the pool)
 #   yevery:    -DMIRSHA_AB_ROUNDS=rounds_asm_y_every (issue-yield s_nop after every 4-cycle op,
 #              the round-1/2 form; other patterns: rounds_asm_y_* in tools/sha256_rounds_asm_ab.h)
+#   latilp:    -DMIRSHA_AB_LAT_ROUNDS=rounds_asm_ilp (lone-wave chains: schedule woven into the rounds)
 #   notail:    -DMIRSHA_AB_NOTAIL       (no final-block tail form: every block through compress_asm)
 #   AB_ONLY="a b" builds only the named variants.
 #   prioN:     -DMIRSHA_PRIO_TOP=N      (block b's rounds at issue priority max(0, N - b), clamped to 3; product 3)
@@ -39,5 +40,6 @@ build spawn -DMIRSHA_AB_SPAWN_THREADS &
 build prio0 -DMIRSHA_PRIO_TOP=0 &
 build yevery -DMIRSHA_AB_ROUNDS=rounds_asm_y_every &
 build notail -DMIRSHA_AB_NOTAIL &
+build latilp -DMIRSHA_AB_LAT_ROUNDS=rounds_asm_ilp &
 wait
 ls -la tools/scratch/*/libmirsha.so
