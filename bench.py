@@ -41,7 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mirbft_amd import Engine, sharding  # noqa: E402
-from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS  # noqa: E402
+from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS, KERNEL_OVERLAP  # noqa: E402
 
 SEED_BASE = 0x6D69726266740000
 # Algorithmic work unit: one 64-byte SHA-256 compression = 1384 int32 VALU ops
@@ -90,7 +90,9 @@ def parse():
     p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive host-API measurement")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"),
                    help="PMC traffic per launch, keyed by kernel_source_key(); written by profiles/profile.sh")
-    p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential"],
+    p.add_argument("--no-overlap-extra", dest="overlap_extra", action="store_false",
+                   help="skip the overlapped-cycles figure (configs 2/3 with a sequential plan)")
+    p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential", "overlap"],
                    help="auto: mirsha_pipeline plan, AUTO mode (fused launch for long chains, else request "
                         "kernel then list kernel); none: plain device API (request kernel, then batch kernel); "
                         "fused / sequential: force a plan mode (A/B)")
@@ -161,14 +163,15 @@ def kernel_source_key(variant):
     return h.hexdigest()[:16]
 
 
-def lookup_traffic(path, key, config):
+def lookup_traffic(path, key, config, kernel):
     """hbm_bytes_per_launch of the dominant kernel for this build, or None."""
     try:
         tf = json.load(open(path))
     except (OSError, ValueError):
         return None, None
     for e in tf.get("entries", []):
-        if e.get("key") == key and int(e.get("config", -1)) == int(config):
+        if (e.get("key") == key and int(e.get("config", -1)) == int(config)
+                and e.get("kernel", "sha256_msgs_kernel") == kernel):
             return e.get("hbm_bytes_per_launch"), e
     return None, None
 
@@ -207,8 +210,15 @@ class BatchWorkload:
         self.d_first = torch.from_numpy(self.first.astype(np.int32)).to(dev)
         self.d_bat = torch.empty((self.nbat, 32), dtype=torch.uint8, device=dev)
         eng.synth_requests_device(self.seed, self.first_req, n, self.data_len, self.d_arena.data_ptr())
-        self.plan = (eng.pipeline(n, self.idx, self.first, np.full(n, stride), mode=a.pipeline)
+        # overlap: each step is ONE launch hashing this cycle's requests and the
+        # previous cycle's batches (mirsha_pipeline_overlap_device) on a
+        # sequential plan; request digests alternate between two buffers.
+        self.overlap = a.pipeline == "overlap"
+        pmode = "sequential" if self.overlap else a.pipeline
+        self.plan = (eng.pipeline(n, self.idx, self.first, np.full(n, stride), mode=pmode)
                      if a.pipeline != "none" else None)
+        self.d_reqs = [self.d_req, torch.empty_like(self.d_req)] if self.overlap else None
+        self.cycle = 0
         self.req_blocks = int(blocks(stride)) * n
         bsz = np.diff(self.first).astype(np.int64) * 32
         self.bat_blocks = int(blocks(bsz).sum())
@@ -217,6 +227,14 @@ class BatchWorkload:
 
     def step(self):
         e = self.eng
+        if self.overlap:
+            cur, prev = self.d_reqs[self.cycle % 2], self.d_reqs[(self.cycle + 1) % 2]
+            e.pipeline_overlap_device(self.plan, self.d_arena.data_ptr(), self.d_arena.numel(), self.d_off.data_ptr(),
+                                      self.d_len.data_ptr(), cur.data_ptr(),
+                                      prev.data_ptr() if self.cycle else 0, self.d_bat.data_ptr())
+            self.d_req = cur  # the last cycle's request digests (self_check)
+            self.cycle += 1
+            return
         if self.plan is not None:
             e.hash_requests_then_batches_device(self.plan, self.d_arena.data_ptr(), self.d_arena.numel(),
                                                 self.d_off.data_ptr(), self.d_len.data_ptr(), self.d_req.data_ptr(),
@@ -233,6 +251,11 @@ class BatchWorkload:
 
     def dominant(self):
         """(kernel name, launches, ms, compressions, algorithmic HBM bytes) of the dominant kernel."""
+        n_o, ms_o = self.eng.kernel_time(KERNEL_OVERLAP)
+        if n_o:
+            # One launch: this cycle's request compressions + the previous cycle's batch chains.
+            hbm = self.n * self.stride + self.n * 32 + int(self.first[-1]) * 32 + self.nbat * 32
+            return "sha256_msgs_overlap_kernel", n_o, ms_o, self.req_blocks + self.bat_blocks, hbm
         n_f, ms_f = self.eng.kernel_time(KERNEL_FUSED)
         if n_f:
             # One launch does the request AND the batch compressions.
@@ -365,12 +388,60 @@ class BatchWorkload:
                 "pipeline": self.a.pipeline if self.plan is None else f"{self.a.pipeline} -> {self.plan.mode_name}",
                 }
 
+    def overlap_cycles(self):
+        """The same plan as overlapped cycles (mirsha_pipeline_overlap_device):
+        ONE launch per cycle hashes the cycle's requests and the previous
+        cycle's batches, as a stream of Ready() cycles pipelines (the state
+        machine batches digests of earlier cycles).  Measured after the
+        headline steps on rank 0: wall time of --steps launches (no events),
+        then the kernel's event time in a second pass."""
+        if self.plan is None or self.plan.mode_name != "sequential" or self.overlap:
+            return None
+        e, steps = self.eng, self.a.steps
+        d_reqs = [self.d_req, torch.empty_like(self.d_req)]
+        state = {"i": 0}
+
+        def launch():
+            i = state["i"]
+            e.pipeline_overlap_device(self.plan, self.d_arena.data_ptr(), self.d_arena.numel(), self.d_off.data_ptr(),
+                                      self.d_len.data_ptr(), d_reqs[i % 2].data_ptr(),
+                                      d_reqs[(i + 1) % 2].data_ptr() if i else 0, self.d_bat.data_ptr())
+            state["i"] = i + 1
+
+        dev = self.d_req.device
+        for _ in range(max(self.a.warmup, 2)):
+            launch()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            launch()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        e.set_timing_mask([KERNEL_OVERLAP])
+        e.set_timing(True)
+        e.reset_timing()
+        for _ in range(steps):
+            launch()
+        torch.cuda.synchronize(dev)
+        e.set_timing(False)
+        n_o, ms_o = e.kernel_time(KERNEL_OVERLAP)
+        e.set_timing_mask(range(32))
+        kms = ms_o / max(n_o, 1)
+        tops = (self.req_blocks + self.bat_blocks) * OPS_PER_COMPRESSION / (kms * 1e-3) / 1e12
+        return {"digests_per_s": self.digests * steps / dt, "ms_per_step": dt / steps * 1e3,
+                "kernel": "sha256_msgs_overlap_kernel", "avg_launch_ms": kms, "frac": tops / VALU_PEAK_TOPS,
+                "note": "one launch per cycle: this cycle's requests + the previous cycle's batch chains "
+                        "(mirsha_pipeline_overlap_device), steady state of a cycle stream; frac over both"}
+
     def extra(self):
         mode = self.plan.mode_name if self.plan is not None else "none"
+        if self.overlap:
+            return {"batch_pass": "overlapped: the previous cycle's batch chains in each cycle's request launch"}
         return {"batch_kernel_avg_ms": self.batch_ms() / self.a.steps,
                 "batch_pass": {"none": "sequential batch kernel (plain device API)",
                                "fused": "fused into the request launch (readiness counters, no second kernel)",
-                               "sequential": "plan: request kernel then batch kernel"}[mode]}
+                               "sequential": "plan: request kernel then batch kernel"}[mode],
+                "overlap_cycles": getattr(self, "ovl", None)}
 
 
 class MixedWorkload:
@@ -721,7 +792,7 @@ def main():
         return el
 
     if a.timed_kernels == "dominant":
-        eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED])
+        eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED, KERNEL_OVERLAP])
     dt = timed(bool(a.events_in_timed_loop))
     if not a.events_in_timed_loop:
         timed(True)
@@ -732,6 +803,11 @@ def main():
         # line's extras); the value and the roofline come from the pass above.
         eng.set_timing_mask(range(32))
         timed(True)
+
+    # Configs 2/3 with a sequential plan: the overlapped-cycles figure, right
+    # behind the timed region too (the chip still at its load clock).
+    if rank == 0 and a.overlap_extra and hasattr(wl, "overlap_cycles"):
+        wl.ovl = wl.overlap_cycles()
 
     # Clock probe right behind the timed region (chip still at its load clock):
     # register-only compressions in the request kernel's round form.
@@ -760,7 +836,7 @@ def main():
     hbm_gbs = hbm_bytes / (ms_per_step_k * 1e-3) / 1e9
 
     tkey = kernel_source_key(a.variant)
-    traffic, tentry = lookup_traffic(a.traffic_file, tkey, a.config)
+    traffic, tentry = lookup_traffic(a.traffic_file, tkey, a.config, kname)
     # Measured ceiling: the probe's register-only compression rate on this box
     # (1,024 SIMDs x 64 lanes per wave-compression) and the clock it ran at.
     measured = None

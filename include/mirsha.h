@@ -86,7 +86,8 @@ int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 /* Per-kernel device-time accounting with HIP events on the launch stream.
  * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator
  * and clock probe, 3 = batch-chain kernel, 4 = fused request -> batch kernel
- * (one persistent launch per run).
+ * (one persistent launch per run), 5 = overlapped-cycles kernel
+ * (mirsha_pipeline_overlap_device).
  * set_timing_mask: bit k on = kernel k is timed while timing is enabled
  * (default: all); each timed launch adds two event records to its stream. */
 int mirsha_ctx_set_timing(mirsha_ctx* ctx, int enable);
@@ -282,6 +283,21 @@ int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t*
 int mirsha_hash_requests_then_batches_device(mirsha_ctx* ctx, mirsha_pipeline* p, const uint8_t* d_arena,
                                              uint64_t arena_len, const uint64_t* d_off, const uint32_t* d_len,
                                              uint8_t* d_req_out, uint8_t* d_batch_out);
+
+/* Overlapped cycles (sequential plans: many short lists, e.g. BatchSize-20
+ * batches).  The state machine batches request digests it already holds, i.e.
+ * results of EARLIER Ready() cycles (sequence.go:154-157), so in a stream of
+ * cycles ONE launch hashes this cycle's requests (d_arena.. -> d_req_out, origin
+ * order, as mirsha_hash_requests_then_batches_device) together with the batch
+ * digests of the previous cycle over ITS request digests d_prev_req (p's lists)
+ * into d_prev_batch_out: the batch chains run beside the request tiles at full
+ * occupancy instead of in a second launch of lone chain waves.  d_req_out ==
+ * NULL: chains only (the last cycle's flush); d_prev_req == NULL: requests
+ * only (the first cycle).  d_prev_req must stay intact until the launch ends
+ * (the context stream orders it).  Asynchronous on the context stream. */
+int mirsha_pipeline_overlap_device(mirsha_ctx* ctx, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len,
+                                   const uint64_t* d_off, const uint32_t* d_len, uint8_t* d_req_out,
+                                   const uint8_t* d_prev_req, uint8_t* d_prev_batch_out);
 
 /* Host helper: order[] = message indices sorted by SHA-256 block count,
  * longest first (stable), so a wave's 64 lanes run equal-length chains.

@@ -86,6 +86,10 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "mirsha_pipeline_overlap_device": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "mirsha_chains_create": (c_int, [c_void_p, c_uint32, POINTER(c_void_p)]),
     "mirsha_chains_destroy": (None, [c_void_p]),
     "mirsha_chains_absorb": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),

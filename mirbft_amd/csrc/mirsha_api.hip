@@ -129,7 +129,7 @@ struct mirsha_ctx {
     // stream, so chunk k's digests return while chunk k+1's bytes go in.
     hipStream_t xin = nullptr, xout = nullptr;
     std::vector<hipEvent_t> xev;  // per-call events (grow-only pool)
-    KernelTimer timers[6];         // msgs, lists, gen, chain, fused, (5: retired)
+    KernelTimer timers[6];         // msgs, lists, gen, chain, fused, overlap
     AsyncSlot slots[kAsyncSlots];
     uint64_t next_ticket = 1;  // ticket of the next submission
     uint64_t done_ticket = 0;  // every ticket <= this one has completed
@@ -1747,6 +1747,40 @@ int mirsha_hash_requests_then_batches_device(mirsha_ctx* c, mirsha_pipeline* p, 
     if (arena_len > MIRSHA_MAX_DEVICE_ARENA_BYTES) return fail(c, MIRSHA_ERANGE, "device arena too large");
     if (int rc = use_device(c)) return rc;
     return plan_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, d_batch_out);
+}
+
+int mirsha_pipeline_overlap_device(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len,
+                                   const uint64_t* d_off, const uint32_t* d_len, uint8_t* d_req_out,
+                                   const uint8_t* d_prev_req, uint8_t* d_prev_batch_out) {
+    if (!c || !p) return MIRSHA_EINVAL;
+    if (p->device != c->device) return fail(c, MIRSHA_EINVAL, "pipeline built for device %d", p->device);
+    if (p->mode != MIRSHA_PIPELINE_SEQUENTIAL)
+        return fail(c, MIRSHA_EINVAL, "overlapped cycles need a sequential plan (short lists)");
+    const bool tiles = d_req_out != nullptr && p->n_req;
+    const bool chains = d_prev_req != nullptr && p->n_lists;
+    if (tiles && (!d_off || !d_len || (!d_arena && arena_len))) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    if (chains && !d_prev_batch_out) return fail(c, MIRSHA_EINVAL, "NULL batch output");
+    if (arena_len > mirsha::kMaxBufferArena) return fail(c, MIRSHA_ERANGE, "overlap: arena > %llu bytes",
+                                                         (unsigned long long)mirsha::kMaxBufferArena);
+    if (p->n_req >= mirsha::kMaxBufferMsgs) return fail(c, MIRSHA_ERANGE, "overlap: %u requests", p->n_req);
+    if (int rc = use_device(c)) return rc;
+    mirsha::OverlapArgs a{};
+    a.arena = d_arena;
+    a.arena_len = tiles ? arena_len : 0;
+    a.off = d_off;
+    a.len = d_len;
+    a.order = p->d_order.as<uint32_t>();
+    a.n_req = tiles ? p->n_req : 0u;
+    a.req_out = d_req_out;
+    a.prev_digests = d_prev_req;
+    a.n_req_prev = p->n_req;
+    a.cidx = p->d_cidx.as<uint32_t>();
+    a.n_entries = p->n_entries;
+    a.cfirst = p->d_cfirst.as<uint32_t>();
+    a.n_lists = p->n_lists;
+    a.list_out = d_prev_batch_out;
+    a.list_waves = chains ? (p->n_lists + 63u) / 64u : 0u;
+    return timed_launch(c, 5, [&] { return mirsha::launch_msgs_overlap(a, c->stream); });
 }
 
 int mirsha_digest_lists(mirsha_ctx* c, const uint8_t* digests, uint32_t n_digests, const uint32_t* idx,

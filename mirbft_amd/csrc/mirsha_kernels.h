@@ -61,6 +61,26 @@ hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32
 // workgroup per 64 lists; for at most kPairMaxGroups groups.
 hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                              const uint32_t* cfirst, uint32_t n_lists, uint8_t* out, hipStream_t s);
+// Overlapped cycles (see mirsha_kernels.hip): this cycle's request tiles and
+// the previous cycle's compacted list chains in one launch.
+struct OverlapArgs {
+    const uint8_t* arena;
+    uint64_t arena_len;
+    const uint64_t* off;
+    const uint32_t* len;
+    const uint32_t* order;  // NULL = identity
+    uint32_t n_req;         // this cycle's requests (0: chains only)
+    uint8_t* req_out;
+    const uint8_t* prev_digests;  // previous cycle's request digests
+    uint32_t n_req_prev;
+    const uint32_t* cidx;
+    uint32_t n_entries;
+    const uint32_t* cfirst;
+    uint32_t n_lists;
+    uint8_t* list_out;
+    uint32_t list_waves;  // (n_lists + 63) / 64, or 0: no chains this launch
+};
+hipError_t launch_msgs_overlap(const OverlapArgs& a, hipStream_t s);
 // Fused request -> list pass (one persistent launch), see mirsha_kernels.hip.
 constexpr uint32_t kFusedChunkBlocks = 2;  // list blocks (4 digests) per readiness chunk
 // Tile queues of the fused launch: queue q holds tiles [q_first[q], q_first[q+1])

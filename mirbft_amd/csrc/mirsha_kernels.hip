@@ -638,6 +638,92 @@ __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_ms
     hash_tile<kLds, kWide>(arena, arena_len, off, len, order, n, out, tile[wv], t, lane);
 }
 
+// ---- overlapped cycles: this cycle's request tiles + the previous cycle's
+// batch chains in ONE launch ------------------------------------------------
+// The state machine batches only request digests it already holds (results of
+// earlier Ready() cycles: sequence.go:154-157 over client_tracker digests), so
+// a stream of cycles pipelines: the launch that hashes cycle i's requests also
+// runs cycle i-1's batch chains (compacted lists over its device-resident
+// request digests, no readiness waits).  Chain waves come first in the grid
+// and run at full occupancy beside the tile waves, at the throughput round
+// form, instead of a second latency-bound launch of lone waves (36 us of a
+// 221 us config-2 step).  Chain wave block b runs at priority
+// 3 - floor(4 b / blocks): a chain is ~2x a request tile's length, so it keeps
+// up with the tiles' progress priorities instead of starving behind the second
+// generation.
+__device__ __forceinline__ uint32_t ld_u32(__amdgpu_buffer_rsrc_t rs, uint32_t off, bool live);
+__device__ __forceinline__ void load_digest(__amdgpu_buffer_rsrc_t rsrc, uint32_t id, bool live, uint4& x0,
+                                            uint4& x1);
+__device__ __forceinline__ void overlap_chain(const uint8_t* __restrict__ digests, uint32_t n_digests,
+                                              const uint32_t* __restrict__ cidx, uint32_t n_entries,
+                                              const uint32_t* __restrict__ cfirst, uint32_t n_lists,
+                                              uint8_t* __restrict__ list_out, uint32_t g, uint32_t lane) {
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t k = g * 64u + lane;
+    const bool valid = k < n_lists;
+    const uint32_t kc = valid ? k : n_lists - 1u;  // unconditional loads (n_lists >= 1)
+    const uint32_t e0_ = cfirst[kc], e1_ = cfirst[kc + 1];
+    const uint32_t e0 = valid ? e0_ : 0u;
+    const uint32_t c = valid ? e1_ - e0_ : 0u;
+    const uint32_t L = 32u * c;
+    const uint32_t nb = valid ? blocks_for_len(L) : 0u;
+    const uint32_t wave_nb = blocks_for_len(32u * wave_max(c));
+    const __amdgpu_buffer_rsrc_t drs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)cidx, (short)0, (int)(4u * n_entries), 0x00020000);
+    uint32_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    // Indices one block ahead; the block's digests are loaded right before its
+    // rounds (the other waves of the SIMD cover the latency; a digest prefetch
+    // would cost 16 VGPRs of the 8-wave budget).
+    uint32_t i0 = ld_u32(irs, 4u * e0, 0u < c), i1 = ld_u32(irs, 4u * (e0 + 1u), 1u < c);
+    for (uint32_t blk = 0; blk < wave_nb; blk++) {
+        const uint32_t d0 = 2u * blk;
+        uint4 x[4];
+        load_digest(drs, i0, d0 < c, x[0], x[1]);
+        load_digest(drs, i1, d0 + 1u < c, x[2], x[3]);
+        i0 = ld_u32(irs, 4u * (e0 + d0 + 2u), d0 + 2u < c);
+        i1 = ld_u32(irs, 4u * (e0 + d0 + 3u), d0 + 3u < c);
+        uint32_t w[16];
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+            const uint32_t di = d0 + (uint32_t)half;
+            const uint4 a = x[2 * half], b = x[2 * half + 1];
+            w[8 * half + 0] = __builtin_bswap32(a.x) | (di == c ? 0x80000000u : 0u);
+            w[8 * half + 1] = __builtin_bswap32(a.y); w[8 * half + 2] = __builtin_bswap32(a.z);
+            w[8 * half + 3] = __builtin_bswap32(a.w); w[8 * half + 4] = __builtin_bswap32(b.x);
+            w[8 * half + 5] = __builtin_bswap32(b.y); w[8 * half + 6] = __builtin_bswap32(b.z);
+            w[8 * half + 7] = __builtin_bswap32(b.w);
+        }
+        if (blk + 1u == nb) {
+            w[14] = L >> 29;
+            w[15] = L << 3;
+        }
+        fixed_prio(3u - min(3u, 4u * blk / wave_nb));
+        if (blk < nb) compress_asm(st, w);
+    }
+    if (valid) {
+        const __amdgpu_buffer_rsrc_t ors =
+            __builtin_amdgcn_make_buffer_rsrc((void*)list_out, (short)0, (int)(32u * n_lists), 0x00020000);
+        store_digest_buf(ors, k, st);
+    }
+}
+
+__global__ __launch_bounds__(64, kMsgOcc) void sha256_msgs_overlap_kernel(OverlapArgs a) {
+    __shared__ uint4 tile[kTileSlots];
+    const uint32_t lane = threadIdx.x;
+    if (blockIdx.x < a.list_waves) {
+        overlap_chain(a.prev_digests, a.n_req_prev, a.cidx, a.n_entries, a.cfirst, a.n_lists, a.list_out,
+                      blockIdx.x, lane);
+        return;
+    }
+    const uint32_t t = blockIdx.x - a.list_waves;
+    if (t * 64u >= a.n_req) return;
+    hash_tile<true, false>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, a.req_out, tile, t, lane);
+}
+
 // Low-occupancy form of the request kernel, for launches of at most one wave
 // per SIMD (a few long messages: e.g. the distinct EpochChange payloads of a
 // deduplicated cycle).  A lone wave's memory latency is not hidden by other
@@ -1531,6 +1617,15 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_kernel<false><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
     else
         sha256_msgs_kernel<true><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_msgs_overlap(const OverlapArgs& a, hipStream_t s) {
+    const uint32_t tiles = (a.n_req + 63u) / 64u;
+    if (a.list_waves + tiles == 0) return hipSuccess;
+    if (a.arena_len > kMaxBufferArena || a.n_req >= kMaxBufferMsgs || (a.list_waves && a.n_lists == 0))
+        return hipErrorInvalidValue;
+    sha256_msgs_overlap_kernel<<<a.list_waves + tiles, 64, 0, s>>>(a);
     return hipGetLastError();
 }
 

@@ -20,6 +20,7 @@ KERNEL_LISTS = 1
 KERNEL_GEN = 2
 KERNEL_CHAIN = 3
 KERNEL_FUSED = 4
+KERNEL_OVERLAP = 5
 ASYNC_SLOTS = 4  # submissions in flight per context (mirsha_submit_slices)
 
 # mirsha_pipeline modes (include/mirsha.h)
@@ -345,6 +346,14 @@ class Engine:
         self._check(self._lib.mirsha_hash_requests_then_batches_device(
             self.ctx, plan.handle, d_arena, arena_len, d_off, d_len, d_req_out, d_batch_out))
 
+    def pipeline_overlap_device(self, plan: "Pipeline", d_arena: int, arena_len: int, d_off: int, d_len: int,
+                                d_req_out: int, d_prev_req: int, d_prev_batch_out: int) -> None:
+        """One launch: this cycle's requests -> d_req_out and the previous cycle's
+        batch digests from d_prev_req -> d_prev_batch_out (0 = none; see mirsha.h)."""
+        self._check(self._lib.mirsha_pipeline_overlap_device(
+            self.ctx, plan.handle, d_arena or None, arena_len, d_off or None, d_len or None, d_req_out or None,
+            d_prev_req or None, d_prev_batch_out or None))
+
     def synth_requests_device(self, seed: int, first: int, count: int, data_len: int, d_arena: int) -> None:
         self._check(self._lib.mirsha_synth_requests_device(self.ctx, seed, first, count, data_len, d_arena))
 
@@ -521,6 +530,7 @@ __all__ = [
     "KERNEL_GEN",
     "KERNEL_CHAIN",
     "KERNEL_FUSED",
+    "KERNEL_OVERLAP",
     "PIPELINE_SEQUENTIAL",
     "PIPELINE_FUSED",
     "PIPELINE_AUTO",

@@ -471,6 +471,79 @@ def test_pipeline_device_full_size(engine, mode, cfg, data_len, n, bs):
     plan.close()
 
 
+@pytest.mark.parametrize("n,cycles", [(50_003, 3), (1 << 20, 2)])
+def test_pipeline_overlap_cycles(engine, n, cycles):
+    """Overlapped cycles (mirsha_pipeline_overlap_device): each launch hashes
+    cycle i's requests and cycle i-1's BatchSize-20 batch digests; a final
+    chains-only launch flushes the last cycle.  Every cycle a different
+    request stream; request and batch digests bit-exact vs the oracle."""
+    torch = _torch()
+    data_len, bs = 256, 20
+    stride = 16 + data_len
+    idx, first = sharding.batch_lists(n, bs)
+    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="sequential")
+    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    d_req = [torch.empty((n, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    want_req = []
+    for i in range(cycles + 1):
+        prev = d_req[(i + 1) % 2].data_ptr() if i else 0
+        if i < cycles:
+            seed = synth.SEED_BASE + 60 + i
+            engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
+            arena = oracle_py.gen_requests(seed, 0, n, data_len)
+            want_req.append(oracle_py.hash_requests(arena, np.arange(n, dtype=np.uint64) * stride,
+                                                    np.full(n, stride), threads=8))
+            d_bat.zero_()
+            torch.cuda.synchronize()
+            engine.pipeline_overlap_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
+                                           d_len.data_ptr(), d_req[i % 2].data_ptr(), prev, d_bat.data_ptr())
+        else:  # flush: the last cycle's batches only
+            d_bat.zero_()
+            torch.cuda.synchronize()
+            engine.pipeline_overlap_device(plan, 0, 0, 0, 0, 0, prev, d_bat.data_ptr())
+        engine.sync()
+        if i < cycles:
+            assert np.array_equal(d_req[i % 2].cpu().numpy(), want_req[i]), f"cycle {i} requests"
+        if i:
+            assert np.array_equal(d_bat.cpu().numpy(), oracle_py.batch_digests(want_req[i - 1], idx, first)), \
+                f"cycle {i - 1} batches"
+    plan.close()
+
+
+def test_pipeline_overlap_irregular_lists(engine):
+    """Overlapped chains over compacted irregular lists (shared, unlisted and
+    null entries, empty and odd lists) of a mixed-length request stream."""
+    torch = _torch()
+    arena, off, lens, idx, first = _irregular(51, 4000, 500, 70, 700)
+    n = lens.size
+    plan = engine.pipeline(n, idx, first, lens, mode="sequential")
+    d_arena = torch.from_numpy(arena).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+    d_req = [torch.empty((n, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    want_req = oracle_py.hash_requests(arena, off, lens)
+    want_bat = oracle_py.batch_digests(want_req, idx, first)
+    torch.cuda.synchronize()
+    engine.pipeline_overlap_device(plan, d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(),
+                                   d_req[0].data_ptr(), 0, d_bat.data_ptr())
+    engine.pipeline_overlap_device(plan, d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(),
+                                   d_req[1].data_ptr(), d_req[0].data_ptr(), d_bat.data_ptr())
+    engine.sync()
+    assert np.array_equal(d_req[0].cpu().numpy(), want_req)
+    assert np.array_equal(d_req[1].cpu().numpy(), want_req)
+    assert np.array_equal(d_bat.cpu().numpy(), want_bat)
+    fused = engine.pipeline(n, idx, first, lens, mode="fused")
+    with pytest.raises(MirshaError):
+        engine.pipeline_overlap_device(fused, d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(),
+                                       d_req[0].data_ptr(), 0, d_bat.data_ptr())
+    fused.close()
+    plan.close()
+
+
 def _irregular(seed, n=3000, n_lists=300, max_list=60, max_len=600):
     rng = np.random.default_rng(seed)
     lens = rng.integers(0, max_len, n).astype(np.uint32)
