@@ -214,7 +214,7 @@ class BatchWorkload:
         # previous cycle's batches (mirsha_pipeline_overlap_device) on a
         # sequential plan; request digests alternate between two buffers.
         self.overlap = a.pipeline == "overlap"
-        pmode = "sequential" if self.overlap else a.pipeline
+        pmode = "auto" if self.overlap else a.pipeline
         self.plan = (eng.pipeline(n, self.idx, self.first, np.full(n, stride), mode=pmode)
                      if a.pipeline != "none" else None)
         self.d_reqs = [self.d_req, torch.empty_like(self.d_req)] if self.overlap else None
@@ -395,8 +395,9 @@ class BatchWorkload:
         machine batches digests of earlier cycles).  Measured after the
         headline steps on rank 0: wall time of --steps launches (no events),
         then the kernel's event time in a second pass."""
-        if self.plan is None or self.plan.mode_name != "sequential" or self.overlap:
+        if self.plan is None or self.overlap:
             return None
+        timer = KERNEL_FUSED if self.plan.mode_name == "fused" else KERNEL_OVERLAP
         e, steps = self.eng, self.a.steps
         d_reqs = [self.d_req, torch.empty_like(self.d_req)]
         state = {"i": 0}
@@ -417,21 +418,23 @@ class BatchWorkload:
             launch()
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
-        e.set_timing_mask([KERNEL_OVERLAP])
+        e.set_timing_mask([timer])
         e.set_timing(True)
         e.reset_timing()
         for _ in range(steps):
             launch()
         torch.cuda.synchronize(dev)
         e.set_timing(False)
-        n_o, ms_o = e.kernel_time(KERNEL_OVERLAP)
+        n_o, ms_o = e.kernel_time(timer)
         e.set_timing_mask(range(32))
         kms = ms_o / max(n_o, 1)
         tops = (self.req_blocks + self.bat_blocks) * OPS_PER_COMPRESSION / (kms * 1e-3) / 1e12
         return {"digests_per_s": self.digests * steps / dt, "ms_per_step": dt / steps * 1e3,
-                "kernel": "sha256_msgs_overlap_kernel", "avg_launch_ms": kms, "frac": tops / VALU_PEAK_TOPS,
+                "kernel": {KERNEL_FUSED: "sha256_fused_paced_kernel"}.get(timer, "sha256_msgs_overlap_kernel"),
+                "avg_launch_ms": kms, "frac": tops / VALU_PEAK_TOPS,
                 "note": "one launch per cycle: this cycle's requests + the previous cycle's batch chains "
-                        "(mirsha_pipeline_overlap_device), steady state of a cycle stream; frac over both"}
+                        "(mirsha_pipeline_overlap_device, on this plan), steady state of a cycle stream; "
+                        "frac over both"}
 
     def extra(self):
         mode = self.plan.mode_name if self.plan is not None else "none"

@@ -284,16 +284,17 @@ int mirsha_hash_requests_then_batches_device(mirsha_ctx* ctx, mirsha_pipeline* p
                                              uint64_t arena_len, const uint64_t* d_off, const uint32_t* d_len,
                                              uint8_t* d_req_out, uint8_t* d_batch_out);
 
-/* Overlapped cycles (sequential plans: many short lists, e.g. BatchSize-20
- * batches).  The state machine batches request digests it already holds, i.e.
+/* Overlapped cycles.  The state machine batches request digests it already holds, i.e.
  * results of EARLIER Ready() cycles (sequence.go:154-157), so in a stream of
  * cycles ONE launch hashes this cycle's requests (d_arena.. -> d_req_out, origin
  * order, as mirsha_hash_requests_then_batches_device) together with the batch
  * digests of the previous cycle over ITS request digests d_prev_req (p's lists)
- * into d_prev_batch_out: the batch chains run beside the request tiles at full
- * occupancy instead of in a second launch of lone chain waves.  d_req_out ==
- * NULL: chains only (the last cycle's flush); d_prev_req == NULL: requests
- * only (the first cycle).  d_prev_req must stay intact until the launch ends
+ * into d_prev_batch_out.  Sequential plans (many short lists, BatchSize 20):
+ * the chains run beside the request tiles at full occupancy instead of in a
+ * second launch of lone chain waves.  Fused plans (long VerifyBatch chains):
+ * the fused launch with its list pairs reading complete digests, so they
+ * never wait on tiles.  d_req_out == NULL: chains only (the last cycle's
+ * flush); d_prev_req == NULL: requests only (the first cycle).  d_prev_req must stay intact until the launch ends
  * (the context stream orders it).  Asynchronous on the context stream. */
 int mirsha_pipeline_overlap_device(mirsha_ctx* ctx, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len,
                                    const uint64_t* d_off, const uint32_t* d_len, uint8_t* d_req_out,

@@ -1097,8 +1097,13 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     return MIRSHA_OK;
 }
 
+// overlap_prev != NULL: overlapped cycles -- the chains hash the PREVIOUS
+// cycle's request digests (complete: no readiness waits) while this launch's
+// tiles hash the current cycle; overlap with overlap_prev == NULL: tiles only
+// (the first cycle).
 int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_t arena_len, const uint64_t* d_off,
-              const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out) {
+              const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out, bool overlap = false,
+              const uint8_t* overlap_prev = nullptr) {
     if (p->n_tiles + p->n_groups == 0) return MIRSHA_OK;
     mirsha::FusedArgs a{};
     a.arena = d_arena;
@@ -1125,9 +1130,10 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.n_req = p->n_req;
     a.n_entries = p->n_entries;
     a.n_lists = p->n_lists;
-    a.epoch = p->epoch + 1ull;
+    a.epoch = overlap ? 0ull : p->epoch + 1ull;  // 0: every readiness target is 0 (no waits)
+    a.list_digests = overlap ? overlap_prev : d_req_out;
     a.n_tiles = p->n_tiles;
-    a.n_groups = p->n_groups;
+    a.n_groups = (overlap && !overlap_prev) ? 0u : p->n_groups;
     a.list_waves = p->list_blocks;
     if (int rc = timed_launch(c, 4, [&] { return mirsha::launch_fused_paced(a, p->grid, p->pace, c->stream); }))
         return rc;
@@ -1754,12 +1760,24 @@ int mirsha_pipeline_overlap_device(mirsha_ctx* c, mirsha_pipeline* p, const uint
                                    const uint8_t* d_prev_req, uint8_t* d_prev_batch_out) {
     if (!c || !p) return MIRSHA_EINVAL;
     if (p->device != c->device) return fail(c, MIRSHA_EINVAL, "pipeline built for device %d", p->device);
-    if (p->mode != MIRSHA_PIPELINE_SEQUENTIAL)
-        return fail(c, MIRSHA_EINVAL, "overlapped cycles need a sequential plan (short lists)");
     const bool tiles = d_req_out != nullptr && p->n_req;
     const bool chains = d_prev_req != nullptr && p->n_lists;
     if (tiles && (!d_off || !d_len || (!d_arena && arena_len))) return fail(c, MIRSHA_EINVAL, "NULL argument");
     if (chains && !d_prev_batch_out) return fail(c, MIRSHA_EINVAL, "NULL batch output");
+    if (p->mode == MIRSHA_PIPELINE_FUSED) {
+        // Long chains (VerifyBatch): the fused launch's tile queues and list
+        // pairs, the pairs over the previous cycle's digests without waits.
+        if (arena_len > MIRSHA_MAX_DEVICE_ARENA_BYTES) return fail(c, MIRSHA_ERANGE, "device arena too large");
+        if (int rc = use_device(c)) return rc;
+        if (tiles)
+            return fused_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, chains ? d_prev_batch_out : nullptr,
+                             true, chains ? d_prev_req : nullptr);
+        if (!chains) return MIRSHA_OK;
+        return timed_launch(c, 1, [&] {  // flush: the last cycle's chains alone, producer/consumer pairs
+            return mirsha::launch_chain_pair(d_prev_req, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
+                                             p->d_cfirst.as<uint32_t>(), p->n_lists, d_prev_batch_out, c->stream);
+        });
+    }
     if (arena_len > mirsha::kMaxBufferArena) return fail(c, MIRSHA_ERANGE, "overlap: arena > %llu bytes",
                                                          (unsigned long long)mirsha::kMaxBufferArena);
     if (p->n_req >= mirsha::kMaxBufferMsgs) return fail(c, MIRSHA_ERANGE, "overlap: %u requests", p->n_req);

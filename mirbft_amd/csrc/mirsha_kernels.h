@@ -115,6 +115,10 @@ struct FusedArgs {
     uint32_t q_first[kFusedMaxQueues + 1];
     uint32_t n_queues;  // = tile waves per SIMD (pace)
     uint32_t steal_own_prio;  // A/B (MIRSHA_FUSED_STEAL_PRIO=1): tiles taken from the last queue keep the taker's priority
+    // Digests the list chains read: req_out (this run's tiles, readiness
+    // waits) or, for overlapped cycles, the previous cycle's request digests
+    // (epoch = 0: no waits).
+    const uint8_t* list_digests;
     uint32_t arena_len, n_req, n_entries, n_lists;
     // Run number of the plan (1, 2, ...): counters are monotone over runs and a
     // chunk is ready at epoch x expected; 64-bit so it never wraps.

@@ -1412,7 +1412,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
     const __amdgpu_buffer_rsrc_t drs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.req_out, (short)0, (int)(32u * a.n_req), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.list_digests, (short)0, (int)(32u * a.n_req), 0x00020000);
     // Slot = this wave's rank among the block's waves on its SIMD (HW_ID), so
     // every SIMD hosts one tile wave per queue, and a list pair spans two
     // SIMDs, whatever the dispatcher's wave placement.

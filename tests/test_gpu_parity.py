@@ -471,17 +471,19 @@ def test_pipeline_device_full_size(engine, mode, cfg, data_len, n, bs):
     plan.close()
 
 
-@pytest.mark.parametrize("n,cycles", [(50_003, 3), (1 << 20, 2)])
-def test_pipeline_overlap_cycles(engine, n, cycles):
+@pytest.mark.parametrize("mode,data_len,bs,n,cycles", [
+    ("sequential", 256, 20, 50_003, 3), ("sequential", 256, 20, 1 << 20, 2),
+    ("fused", 4096, 500, 16_411, 3), ("fused", 4096, 500, 1 << 18, 2)])
+def test_pipeline_overlap_cycles(engine, mode, data_len, bs, n, cycles):
     """Overlapped cycles (mirsha_pipeline_overlap_device): each launch hashes
-    cycle i's requests and cycle i-1's BatchSize-20 batch digests; a final
-    chains-only launch flushes the last cycle.  Every cycle a different
-    request stream; request and batch digests bit-exact vs the oracle."""
+    cycle i's requests and cycle i-1's batch digests (BatchSize 20 on a
+    sequential plan, VerifyBatch 500 on a fused plan); a final chains-only
+    launch flushes the last cycle.  Every cycle a different request stream;
+    request and batch digests bit-exact vs the oracle."""
     torch = _torch()
-    data_len, bs = 256, 20
     stride = 16 + data_len
     idx, first = sharding.batch_lists(n, bs)
-    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="sequential")
+    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode=mode)
     d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
     d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
     d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
@@ -536,10 +538,20 @@ def test_pipeline_overlap_irregular_lists(engine):
     assert np.array_equal(d_req[0].cpu().numpy(), want_req)
     assert np.array_equal(d_req[1].cpu().numpy(), want_req)
     assert np.array_equal(d_bat.cpu().numpy(), want_bat)
+    # the same two cycles on a fused plan (list pairs over the previous digests)
     fused = engine.pipeline(n, idx, first, lens, mode="fused")
-    with pytest.raises(MirshaError):
-        engine.pipeline_overlap_device(fused, d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(),
-                                       d_req[0].data_ptr(), 0, d_bat.data_ptr())
+    d_bat.zero_()
+    torch.cuda.synchronize()
+    engine.pipeline_overlap_device(fused, d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(),
+                                   d_req[0].data_ptr(), d_req[1].data_ptr(), d_bat.data_ptr())
+    engine.sync()
+    assert np.array_equal(d_req[0].cpu().numpy(), want_req)
+    assert np.array_equal(d_bat.cpu().numpy(), want_bat)
+    fused.status()
+    # an ordinary fused run on the same plan afterwards (readiness epochs kept)
+    for req, lst in _plan_run(engine, fused, arena, off, lens, first.size - 1, runs=1):
+        assert np.array_equal(req, want_req)
+        assert np.array_equal(lst, want_bat)
     fused.close()
     plan.close()
 
