@@ -1798,6 +1798,7 @@ int mirsha_pipeline_overlap_device(mirsha_ctx* c, mirsha_pipeline* p, const uint
     a.n_lists = p->n_lists;
     a.list_out = d_prev_batch_out;
     a.list_waves = chains ? (p->n_lists + 63u) / 64u : 0u;
+    if (const char* e = getenv("MIRSHA_OVERLAP_CHAIN_PRIO")) a.chain_prio = (uint32_t)atoi(e) & 3u;
     return timed_launch(c, 5, [&] { return mirsha::launch_msgs_overlap(a, c->stream); });
 }
 

@@ -79,6 +79,7 @@ struct OverlapArgs {
     uint32_t n_lists;
     uint8_t* list_out;
     uint32_t list_waves;  // (n_lists + 63) / 64, or 0: no chains this launch
+    uint32_t chain_prio;  // A/B (MIRSHA_OVERLAP_CHAIN_PRIO): 0 by fraction of the chain, 1 = 3 - block, 2 = 3, 3 = 1
 };
 hipError_t launch_msgs_overlap(const OverlapArgs& a, hipStream_t s);
 // Fused request -> list pass (one persistent launch), see mirsha_kernels.hip.

@@ -657,7 +657,8 @@ __device__ __forceinline__ void load_digest(__amdgpu_buffer_rsrc_t rsrc, uint32_
 __device__ __forceinline__ void overlap_chain(const uint8_t* __restrict__ digests, uint32_t n_digests,
                                               const uint32_t* __restrict__ cidx, uint32_t n_entries,
                                               const uint32_t* __restrict__ cfirst, uint32_t n_lists,
-                                              uint8_t* __restrict__ list_out, uint32_t g, uint32_t lane) {
+                                              uint8_t* __restrict__ list_out, uint32_t g, uint32_t lane,
+                                              uint32_t prio_mode) {
     __builtin_amdgcn_s_setprio(3);
     const uint32_t k = g * 64u + lane;
     const bool valid = k < n_lists;
@@ -701,7 +702,10 @@ __device__ __forceinline__ void overlap_chain(const uint8_t* __restrict__ digest
             w[14] = L >> 29;
             w[15] = L << 3;
         }
-        fixed_prio(3u - min(3u, 4u * blk / wave_nb));
+        fixed_prio(prio_mode == 0u   ? 3u - min(3u, 4u * blk / wave_nb)
+                   : prio_mode == 1u ? 3u - min(3u, blk)
+                   : prio_mode == 2u ? 3u
+                                     : 1u);
         if (blk < nb) compress_asm(st, w);
     }
     if (valid) {
@@ -716,7 +720,7 @@ __global__ __launch_bounds__(64, kMsgOcc) void sha256_msgs_overlap_kernel(Overla
     const uint32_t lane = threadIdx.x;
     if (blockIdx.x < a.list_waves) {
         overlap_chain(a.prev_digests, a.n_req_prev, a.cidx, a.n_entries, a.cfirst, a.n_lists, a.list_out,
-                      blockIdx.x, lane);
+                      blockIdx.x, lane, a.chain_prio);
         return;
     }
     const uint32_t t = blockIdx.x - a.list_waves;
