@@ -35,6 +35,7 @@ constexpr uint32_t kFusedMaxListWaves = 64;      // list groups (64 chains each)
 constexpr uint32_t kFusedMaxListBlocks = 32;     // list CUs (one producer / consumer pair each)
 constexpr uint32_t kFusedMinChainBlocks = 64;    // AUTO picks the fused launch from this chain length
 constexpr uint32_t kFusedDefaultPace = 4;        // tile waves (= tile queues) per SIMD
+constexpr uint32_t kFusedDefaultListTiles = 1;   // FusedArgs::list_tiles (fused_build; profiles/r02au, r02av)
 
 struct DevBuf {
     void* p = nullptr;
@@ -153,6 +154,10 @@ struct mirsha_pipeline {
     std::vector<uint32_t> tadj_first, tadj, cbase, expected;
     uint32_t n_tiles = 0, n_groups = 0, n_counters = 0, grid = 0;
     uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
+    uint32_t list_tiles = 0;  // FusedArgs::list_tiles
+    // Failing ticket claims per run on each queue: the waves whose own queue it
+    // is (q < last), every claiming wave (last).
+    uint32_t q_fail[mirsha::kFusedMaxQueues] = {};
     uint64_t tile_base[mirsha::kFusedMaxQueues] = {};
     uint32_t q_first[mirsha::kFusedMaxQueues + 1] = {};  // tile queues (fused_build)
     uint64_t epoch = 0;  // completed runs of a fused plan
@@ -1055,13 +1060,32 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
         p->pace = std::min<uint32_t>(mirsha::kPacedMaxPace, std::max<uint32_t>(1u, (uint32_t)atoi(e)));
     // one list pair per group, up to kFusedMaxListBlocks CUs (more groups: each pair takes several)
     p->list_blocks = std::min<uint32_t>(std::min<uint32_t>(p->n_groups, kFusedMaxListBlocks), cus / 8u);
-    const uint32_t tile_blocks =
-        std::max<uint32_t>(1, std::min<uint32_t>(cus - p->list_blocks, (p->n_tiles + 4u * p->pace - 1u) / (4u * p->pace)));
-    p->tile_waves = tile_blocks * 4u * p->pace;
-    p->grid = p->list_blocks + tile_blocks;
-    const uint32_t W = 4u * tile_blocks;  // tile waves per slot
-    for (uint32_t q = 0; q < p->pace; q++) p->q_first[q] = std::min<uint32_t>(p->n_tiles, q * W);
-    p->q_first[p->pace] = p->n_tiles;
+    // List blocks' other waves as tile waves (MIRSHA_FUSED_LIST_TILES, A/B):
+    // config 3's 4,096 tiles otherwise leave 144 as a fifth tile on the 988
+    // SIMDs of the tile blocks.
+    p->list_tiles = kFusedDefaultListTiles;
+    if (const char* e = getenv("MIRSHA_FUSED_LIST_TILES")) p->list_tiles = std::min<uint32_t>(2u, (uint32_t)atoi(e));
+    if (p->list_blocks == 0) p->list_tiles = 0;
+    const uint32_t LB = p->list_blocks, P = p->pace;
+    // tile waves of one list block per slot s (pair: slot 0 on SIMDs 0 and 1)
+    auto lb_slot = [&](uint32_t s) -> uint32_t {
+        return p->list_tiles == 0u ? 0u : p->list_tiles == 1u ? 2u : (s == 0u ? 2u : 4u);
+    };
+    uint32_t lb_tiles = 0;
+    for (uint32_t s = 0; s < P; s++) lb_tiles += lb_slot(s);
+    const uint32_t tile_blocks = std::max<uint32_t>(
+        1, std::min<uint32_t>(cus - LB, (p->n_tiles - std::min(p->n_tiles, LB * lb_tiles) + 4u * P - 1u) / (4u * P)));
+    p->tile_waves = tile_blocks * 4u * P + LB * lb_tiles;
+    p->grid = LB + tile_blocks;
+    // Queue q = the next (waves of slot q) tiles in needed-at order; the last takes the rest.
+    uint32_t at = 0;
+    for (uint32_t q = 0; q < P; q++) {
+        p->q_first[q] = std::min<uint32_t>(p->n_tiles, at);
+        p->q_fail[q] = 4u * tile_blocks + LB * lb_slot(q);
+        at += p->q_fail[q];
+    }
+    p->q_first[P] = p->n_tiles;
+    p->q_fail[P - 1u] = p->tile_waves + (p->list_tiles ? 2u * LB : 0u);  // + the pair waves after their chains
     // Device copies.
     auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
         HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
@@ -1126,6 +1150,7 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     for (uint32_t q = 0; q <= mirsha::kFusedMaxQueues; q++) a.q_first[q] = p->q_first[std::min(q, p->pace)];
     a.n_queues = p->pace;
     a.steal_own_prio = getenv_flag("MIRSHA_FUSED_STEAL_PRIO") ? 1u : 0u;
+    a.list_tiles = p->list_tiles;
     a.arena_len = (uint32_t)arena_len;
     a.n_req = p->n_req;
     a.n_entries = p->n_entries;
@@ -1138,10 +1163,9 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     if (int rc = timed_launch(c, 4, [&] { return mirsha::launch_fused_paced(a, p->grid, p->pace, c->stream); }))
         return rc;
     // Every tile wave made exactly one failing claim on its own queue and one on
-    // the last queue (the same one for the last slot).
-    const uint32_t last = p->pace - 1u, W = p->tile_waves / p->pace;
-    for (uint32_t q = 0; q < p->pace; q++)
-        p->tile_base[q] += (p->q_first[q + 1] - p->q_first[q]) + (q == last ? p->tile_waves : W);
+    // the last queue (the same one for the last slot); the pair waves of
+    // list_tiles plans one on the last queue.
+    for (uint32_t q = 0; q < p->pace; q++) p->tile_base[q] += (p->q_first[q + 1] - p->q_first[q]) + p->q_fail[q];
     p->epoch++;
     return MIRSHA_OK;
 }

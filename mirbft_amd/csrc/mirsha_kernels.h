@@ -116,6 +116,10 @@ struct FusedArgs {
     uint32_t q_first[kFusedMaxQueues + 1];
     uint32_t n_queues;  // = tile waves per SIMD (pace)
     uint32_t steal_own_prio;  // A/B (MIRSHA_FUSED_STEAL_PRIO=1): tiles taken from the last queue keep the taker's priority
+    // Tile waves in LIST blocks (MIRSHA_FUSED_LIST_TILES): 0 = none (the pair
+    // is alone on its CU), 1 = the waves on SIMDs 2-3, 2 = every wave but the
+    // pair; with 1 and 2 the pair waves take last-queue tiles after their chains.
+    uint32_t list_tiles;
     // Digests the list chains read: req_out (this run's tiles, readiness
     // waits) or, for overlapped cycles, the previous cycle's request digests
     // (epoch = 0: no waits).
@@ -127,9 +131,11 @@ struct FusedArgs {
     uint32_t n_tiles, n_groups, list_waves;
 };
 // list_waves = number of list BLOCKS (first in the grid); one block per CU
-// (kPacedLds of LDS: the tile waves' 4 KiB staging tiles, and enough to keep
-// any second block off the CU), `pace` tile waves per SIMD in tile blocks.
-constexpr uint32_t kPacedLds = 96u * 1024u;
+// (kPacedLds of LDS: 16 waves' 4 KiB staging tiles, then a list block's pair
+// ring; more than half the CU's LDS keeps any second block off the CU), `pace`
+// tile waves per SIMD.
+constexpr uint32_t kPacedRingOff = 64u * 1024u;
+constexpr uint32_t kPacedLds = 97u * 1024u;
 constexpr uint32_t kPacedMaxPace = 4;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words

@@ -1396,8 +1396,9 @@ __device__ __forceinline__ void fused_list_produce(const FusedArgs& a, __amdgpu_
 }
 
 // Block = 4 x pace waves (pace per SIMD; wave w on SIMD w % 4), one block per
-// CU (kPacedLds of LDS).  List blocks [0, list_blocks) run one chain wave per
-// SIMD ALONE on their CU (waves 4.. of a list block exit at once).  Tile
+// CU (kPacedLds of LDS).  List blocks [0, list_blocks) run a chain pair on
+// SIMDs 0 and 1; their other waves exit at once or, with list_tiles, serve
+// the tile queues like a tile block's (FusedArgs::list_tiles).  Tile
 // blocks fill the other CUs with `pace` tile waves per SIMD, one per tile
 // QUEUE: the wave of slot q = w / 4 serves queue q (tiles in needed-at order,
 // queue 0 the earliest) at issue priority prio_of(q), so on every SIMD the
@@ -1421,7 +1422,9 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // every SIMD hosts one tile wave per queue, and a list pair spans two
     // SIMDs, whatever the dispatcher's wave placement.
     __shared__ uint32_t simd_waves[4];
-    FusedPairRing& ring = *reinterpret_cast<FusedPairRing*>(paced_lds);
+    static_assert(kPacedRingOff + sizeof(FusedPairRing) <= kPacedLds && kPacedRingOff >= 4096u * kPacedMaxPace * 4u,
+                  "paced LDS: staging tiles, then the pair ring");
+    FusedPairRing& ring = *reinterpret_cast<FusedPairRing*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedRingOff);
     const bool list_block = blockIdx.x < a.list_waves;  // list_waves carries the number of LIST BLOCKS
     if (threadIdx.x < 4u) simd_waves[threadIdx.x] = 0u;
     if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = 0u;
@@ -1432,8 +1435,10 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     uint32_t slot = 0u;
     if (lane == 0u) slot = atomicAdd(&simd_waves[simd], 1u);
     slot = (uint32_t)__shfl((int)slot, 0, 64);
-    if (list_block) {  // groups blockIdx.x, + list blocks, ...: producer on SIMD 0, consumer on SIMD 1
-        if (slot != 0u || simd > 1u) return;
+    bool own = true;
+    if (list_block && (slot != 0u || simd > 1u)) {  // not the pair: a tile wave, or idle
+        if (a.list_tiles == 0u || (a.list_tiles == 1u && simd <= 1u)) return;
+    } else if (list_block) {  // groups blockIdx.x, + list blocks, ...: producer on SIMD 0, consumer on SIMD 1
         __builtin_amdgcn_s_setprio(3);
         uint32_t seq = 0u;
         if (simd == 0u) {
@@ -1444,12 +1449,12 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
         } else {
             for (uint32_t g = blockIdx.x; g < a.n_groups; g += a.list_waves) fused_list_consume(a, ring, g, lane, seq);
         }
-        return;
+        if (a.list_tiles == 0u) return;
+        own = false;  // chains done: tiles left in the last queue (the overflow)
     }
     uint4* my = paced_lds + 256u * wv;  // the wave's 4 KiB staging tile
     const uint32_t last = a.n_queues - 1u;
     const uint32_t q = min(slot, last);
-    bool own = true;
     while (true) {
         const uint32_t qq = own ? q : last;
         const uint64_t t = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) - a.tile_base[qq] + a.q_first[qq];

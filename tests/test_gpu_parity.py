@@ -590,11 +590,13 @@ def test_pipeline_irregular_lists(engine, monkeypatch, env_mode):
     (34, 1, 3, 40, 10),              # one request, repeated in every list
     (35, 5000, 2, 0, 2000),          # only empty lists (no entries): padding block only
 ])
-@pytest.mark.parametrize("pace", [1, 2, 4])
-def test_fused_plan_irregular(engine, monkeypatch, pace, seed, n, n_lists, max_list, max_len):
+@pytest.mark.parametrize("pace,list_tiles", [(1, 0), (2, 0), (4, 0), (1, 2), (3, 1), (4, 1), (4, 2)])
+def test_fused_plan_irregular(engine, monkeypatch, pace, list_tiles, seed, n, n_lists, max_list, max_len):
     """Fused plan (device API) on irregular shapes, three runs on one plan (the
-    tile queues' tickets carried across runs), 1, 2 or 4 tile queues."""
+    tile queues' tickets carried across runs), 1-4 tile queues, list blocks
+    with and without tile waves."""
     monkeypatch.setenv("MIRSHA_FUSED_PACE", str(pace))
+    monkeypatch.setenv("MIRSHA_FUSED_LIST_TILES", str(list_tiles))
     arena, off, lens, idx, first = _irregular(seed, n, n_lists, max(max_list, 1), max_len)
     if max_list == 0:
         first = np.zeros(n_lists + 1, dtype=np.uint32)
@@ -605,6 +607,53 @@ def test_fused_plan_irregular(engine, monkeypatch, pace, seed, n, n_lists, max_l
     for req, lst in _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=3):
         assert np.array_equal(req, want_req)
         assert np.array_equal(lst, want_lst)
+    plan.close()
+
+
+@pytest.mark.parametrize("list_tiles", [0, 1, 2])
+def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
+    """Config 3 at full size (2^18 x 4 KB, VerifyBatch 500) on fused plans
+    whose list blocks also run tile waves (MIRSHA_FUSED_LIST_TILES): two
+    ordinary runs, then two overlapped cycles and the flush, bit-exact."""
+    torch = _torch()
+    monkeypatch.setenv("MIRSHA_FUSED_LIST_TILES", str(list_tiles))
+    n, data_len, bs = 1 << 18, 4096, 500
+    stride = 16 + data_len
+    seed = synth.SEED_BASE + 3
+    idx, first = sharding.batch_lists(n, bs)
+    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="fused")
+    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    d_req = [torch.empty((n, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
+    arena = oracle_py.gen_requests(seed, 0, n, data_len)
+    want_req = oracle_py.hash_requests(arena, np.arange(n, dtype=np.uint64) * stride, np.full(n, stride), threads=8)
+    want_bat = oracle_py.batch_digests(want_req, idx, first)
+    args = (d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr())
+    for _ in range(2):
+        d_req[0].zero_()
+        d_bat.zero_()
+        engine.hash_requests_then_batches_device(plan, *args, d_req[0].data_ptr(), d_bat.data_ptr())
+        plan.status()
+        assert np.array_equal(d_req[0].cpu().numpy(), want_req)
+        assert np.array_equal(d_bat.cpu().numpy(), want_bat)
+    for i in range(3):  # two cycles of the same stream, then the flush
+        d_bat.zero_()
+        torch.cuda.synchronize()
+        prev = d_req[(i + 1) % 2].data_ptr() if i else 0
+        if i < 2:
+            d_req[i % 2].zero_()
+            engine.pipeline_overlap_device(plan, *args, d_req[i % 2].data_ptr(), prev, d_bat.data_ptr())
+        else:
+            engine.pipeline_overlap_device(plan, 0, 0, 0, 0, 0, prev, d_bat.data_ptr())
+        engine.sync()
+        if i < 2:
+            assert np.array_equal(d_req[i % 2].cpu().numpy(), want_req), f"cycle {i} requests"
+        if i:
+            assert np.array_equal(d_bat.cpu().numpy(), want_bat), f"cycle {i - 1} batches"
+    plan.status()
     plan.close()
 
 
