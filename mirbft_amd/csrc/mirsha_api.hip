@@ -155,10 +155,6 @@ struct mirsha_pipeline {
     uint32_t n_tiles = 0, n_groups = 0, n_counters = 0, grid = 0;
     uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
     uint32_t list_tiles = 0;  // FusedArgs::list_tiles
-    // Failing ticket claims per run on each queue: the waves whose own queue it
-    // is (q < last), every claiming wave (last).
-    uint32_t q_fail[mirsha::kFusedMaxQueues] = {};
-    uint64_t tile_base[mirsha::kFusedMaxQueues] = {};
     uint32_t q_first[mirsha::kFusedMaxQueues + 1] = {};  // tile queues (fused_build)
     uint64_t epoch = 0;  // completed runs of a fused plan
     DevBuf d_tadj_first, d_tadj, d_cbase, d_expected, d_counters, d_ctl, d_trace;
@@ -1081,11 +1077,9 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     uint32_t at = 0;
     for (uint32_t q = 0; q < P; q++) {
         p->q_first[q] = std::min<uint32_t>(p->n_tiles, at);
-        p->q_fail[q] = 4u * tile_blocks + LB * lb_slot(q);
-        at += p->q_fail[q];
+        at += 4u * tile_blocks + LB * lb_slot(q);
     }
     p->q_first[P] = p->n_tiles;
-    p->q_fail[P - 1u] = p->tile_waves + (p->list_tiles ? 2u * LB : 0u);  // + the pair waves after their chains
     // Device copies.
     auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
         HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
@@ -1108,7 +1102,6 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     HIP_TRY(c, p->d_ctl.ensure(8ull * mirsha::kCtlWords));
     HIP_TRY(c, hipMemsetAsync(p->d_ctl.p, 0, 8ull * mirsha::kCtlWords, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    for (uint64_t& b : p->tile_base) b = 0;
     p->epoch = 0;
     const char* tr = getenv("MIRSHA_FUSED_TRACE");
     p->trace = tr && atoi(tr) != 0;
@@ -1146,7 +1139,6 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.ctl = p->d_ctl.as<unsigned long long>();
     a.trace = p->trace ? p->d_trace.as<unsigned long long>() : nullptr;
     a.n_counters = p->n_counters;
-    for (uint32_t q = 0; q < mirsha::kFusedMaxQueues; q++) a.tile_base[q] = p->tile_base[q];
     for (uint32_t q = 0; q <= mirsha::kFusedMaxQueues; q++) a.q_first[q] = p->q_first[std::min(q, p->pace)];
     a.n_queues = p->pace;
     a.steal_own_prio = getenv_flag("MIRSHA_FUSED_STEAL_PRIO") ? 1u : 0u;
@@ -1162,10 +1154,6 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.list_waves = p->list_blocks;
     if (int rc = timed_launch(c, 4, [&] { return mirsha::launch_fused_paced(a, p->grid, p->pace, c->stream); }))
         return rc;
-    // Every tile wave made exactly one failing claim on its own queue and one on
-    // the last queue (the same one for the last slot); the pair waves of
-    // list_tiles plans one on the last queue.
-    for (uint32_t q = 0; q < p->pace; q++) p->tile_base[q] += (p->q_first[q + 1] - p->q_first[q]) + p->q_fail[q];
     p->epoch++;
     return MIRSHA_OK;
 }

@@ -88,8 +88,9 @@ constexpr uint32_t kFusedChunkBlocks = 2;  // list blocks (4 digests) per readin
 // in needed-at order and is served first by the tile waves of slot q on every
 // SIMD, at issue priority prio_of(q) (earliest-needed tiles win issue).
 constexpr uint32_t kFusedMaxQueues = 4;
-// ctl words (u64): tile tickets at kCtlTileTicket + 16 q, error flag (one 128-B line each)
-constexpr uint32_t kCtlTileTicket = 0, kCtlError = 64, kCtlWords = 80;
+// ctl words (u64, one 128-B line each): tile tickets at kCtlTileTicket + 16 q,
+// error flag, retired-wave count (the launch's last wave resets the tickets)
+constexpr uint32_t kCtlTileTicket = 0, kCtlError = 64, kCtlDone = 80, kCtlWords = 96;
 struct FusedArgs {
     const uint8_t* arena;
     const uint64_t* off;
@@ -112,7 +113,6 @@ struct FusedArgs {
     // n_groups + ctr]; per list group its end at [3 n_tiles + n_counters + g].
     unsigned long long* trace;
     uint32_t n_counters;
-    unsigned long long tile_base[kFusedMaxQueues];
     uint32_t q_first[kFusedMaxQueues + 1];
     uint32_t n_queues;  // = tile waves per SIMD (pace)
     uint32_t steal_own_prio;  // A/B (MIRSHA_FUSED_STEAL_PRIO=1): tiles taken from the last queue keep the taker's priority

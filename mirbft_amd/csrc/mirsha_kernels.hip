@@ -715,7 +715,12 @@ __device__ __forceinline__ void overlap_chain(const uint8_t* __restrict__ digest
     }
 }
 
-__global__ __launch_bounds__(64, kMsgOcc) void sha256_msgs_overlap_kernel(OverlapArgs a) {
+// Occupancy bound 7 (72 VGPRs allowed): at the bound 8 the chain and tile
+// roles spilled two VGPRs and five SGPRs to scratch (12 B per lane); at 7 the
+// allocator fits them in 64 VGPRs with no spill, so the launch still runs 8
+// waves per SIMD.
+constexpr uint32_t kOverlapOcc = 7;
+__global__ __launch_bounds__(64, kOverlapOcc) void sha256_msgs_overlap_kernel(OverlapArgs a) {
     __shared__ uint4 tile[kTileSlots];
     const uint32_t lane = threadIdx.x;
     if (blockIdx.x < a.list_waves) {
@@ -1194,15 +1199,32 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
 // launch cannot deadlock; a 2 s watchdog per wait raises the error flag
 // instead of hanging if that invariant is ever broken.
 //
-// Tickets are monotone 64-bit counters shared by every run of a plan: each
-// claiming wave makes exactly one failing claim per run, so run r's base is
-// the host-tracked sum of (items + claiming waves) over earlier runs.
+// Tile tickets start every run at 0: each wave of the launch retires once
+// (fused_retire), and the last one resets them, after every claim of the run
+// (each wave's claims complete before its retire count), so no host bookkeeping depends on
+// how many waves claimed or where the dispatcher placed them.
 __device__ __forceinline__ uint64_t claim(unsigned long long* ctr, uint32_t lane) {
     unsigned long long v = 0;
     if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, 0, 64);
     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), 0, 64);
     return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void fused_retire(unsigned long long* ctl, uint32_t lane) {
+    if (lane != 0u) return;
+    const unsigned long long total = (unsigned long long)gridDim.x * (blockDim.x >> 6);
+    // Relaxed: every claim this wave made returned its value (the wave branched
+    // on it) before this add was issued, and device-scope atomics are
+    // performed at one point past the XCDs' L2s (an acq_rel add cost each of
+    // config 3's ~4,000 waves an L2 writeback: +70 us, profiles/r02ay).
+    const unsigned long long old =
+        __hip_atomic_fetch_add(ctl + kCtlDone, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old + 1ull == total) {
+        for (uint32_t q = 0; q < kFusedMaxQueues; q++)
+            __hip_atomic_store(ctl + kCtlTileTicket + 16u * q, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(ctl + kCtlDone, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __device__ __forceinline__ uint64_t poll_counter(const unsigned long long* ctr) {
@@ -1435,9 +1457,9 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     uint32_t slot = 0u;
     if (lane == 0u) slot = atomicAdd(&simd_waves[simd], 1u);
     slot = (uint32_t)__shfl((int)slot, 0, 64);
-    bool own = true;
+    bool own = true, tiles = true;
     if (list_block && (slot != 0u || simd > 1u)) {  // not the pair: a tile wave, or idle
-        if (a.list_tiles == 0u || (a.list_tiles == 1u && simd <= 1u)) return;
+        tiles = !(a.list_tiles == 0u || (a.list_tiles == 1u && simd <= 1u));
     } else if (list_block) {  // groups blockIdx.x, + list blocks, ...: producer on SIMD 0, consumer on SIMD 1
         __builtin_amdgcn_s_setprio(3);
         uint32_t seq = 0u;
@@ -1449,15 +1471,15 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
         } else {
             for (uint32_t g = blockIdx.x; g < a.n_groups; g += a.list_waves) fused_list_consume(a, ring, g, lane, seq);
         }
-        if (a.list_tiles == 0u) return;
+        tiles = a.list_tiles != 0u;
         own = false;  // chains done: tiles left in the last queue (the overflow)
     }
     uint4* my = paced_lds + 256u * wv;  // the wave's 4 KiB staging tile
     const uint32_t last = a.n_queues - 1u;
     const uint32_t q = min(slot, last);
-    while (true) {
+    while (tiles) {
         const uint32_t qq = own ? q : last;
-        const uint64_t t = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) - a.tile_base[qq] + a.q_first[qq];
+        const uint64_t t = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) + a.q_first[qq];
         if (t >= a.q_first[qq + 1]) {
             if (own && qq != last) {
                 own = false;
@@ -1480,6 +1502,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
         for (uint32_t j = j0 + lane; j < j1; j += 64u)
             __hip_atomic_fetch_add(a.counters + a.tadj[j], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    fused_retire(a.ctl, lane);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
