@@ -1220,12 +1220,30 @@ void pipeline_free(mirsha_pipeline* p) {
 
 
 // Validates a slice-list request set and returns each request's total length.
-int slice_lengths(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
-                  const uint32_t* slice_first, uint32_t n, const uint8_t* out, std::vector<uint32_t>& len) {
+// The first request with a per-request slice error (err[i]: 0 ok, 1 not
+// monotone, 2 NULL slice, 3 too long), reported as the call's error.
+int slice_errors(mirsha_ctx* c, const uint8_t* err, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+        if (err[i] == 1) return fail(c, MIRSHA_EINVAL, "slice_first not monotone at request %u", i);
+        if (err[i] == 2) return fail(c, MIRSHA_EINVAL, "request %u has a NULL slice", i);
+        if (err[i] == 3) return fail(c, MIRSHA_ERANGE, "request %u exceeds %u bytes", i, MIRSHA_MAX_MESSAGE_BYTES);
+    }
+    return MIRSHA_OK;
+}
+
+// The call-level checks every slice submission makes first.
+int slice_args(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len, const uint32_t* slice_first,
+               uint32_t n, const uint8_t* out) {
     if (!slice_first || !out) return fail(c, MIRSHA_EINVAL, "NULL argument");
     if (slice_first[0] != 0) return fail(c, MIRSHA_EINVAL, "slice_first[0] must be 0");
+    if (slice_first[n] && (!slice_ptr || !slice_len)) return fail(c, MIRSHA_EINVAL, "NULL slice arrays");
+    return MIRSHA_OK;
+}
+
+int slice_lengths(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
+                  const uint32_t* slice_first, uint32_t n, const uint8_t* out, std::vector<uint32_t>& len) {
+    if (int rc = slice_args(c, slice_ptr, slice_len, slice_first, n, out)) return rc;
     const uint32_t ns = slice_first[n];
-    if (ns && (!slice_ptr || !slice_len)) return fail(c, MIRSHA_EINVAL, "NULL slice arrays");
     len.resize(n);
     // err[i]: 0 ok, 1 not monotone, 2 NULL slice, 3 too long (first error reported)
     std::vector<uint8_t> err(n, 0);
@@ -1242,12 +1260,7 @@ int slice_lengths(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t
             len[i] = (uint32_t)L;
         }
     });
-    for (uint32_t i = 0; i < n; i++) {
-        if (err[i] == 1) return fail(c, MIRSHA_EINVAL, "slice_first not monotone at request %u", i);
-        if (err[i] == 2) return fail(c, MIRSHA_EINVAL, "request %u has a NULL slice", i);
-        if (err[i] == 3) return fail(c, MIRSHA_ERANGE, "request %u exceeds %u bytes", i, MIRSHA_MAX_MESSAGE_BYTES);
-    }
-    return MIRSHA_OK;
+    return slice_errors(c, err.data(), n);
 }
 
 // Copies a completed submission's digests to the caller, in origin order.
@@ -1284,8 +1297,32 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     if (flags & ~MIRSHA_SUBMIT_DEDUP) return fail(c, MIRSHA_EINVAL, "unknown submit flags 0x%x", flags);
     auto t0 = Clock::now();
     for (double& x : c->prof) x = 0.0;
+    // Which requests reach the GPU: all, or one per distinct content.  With
+    // dedup the fingerprint heads (every one of them a final representative)
+    // are packed and queued first; the byte-for-byte confirmation of the
+    // duplicates then runs on the host while the GPU hashes the heads, and
+    // representatives found only there (fingerprint collisions, rare) follow
+    // in a second launch.  The fingerprints are taken in the validation walk
+    // over the slice arrays (dedup_candidates_checked): one pass, not two.
+    const bool dedup = (flags & MIRSHA_SUBMIT_DEDUP) && n > 1;
     std::vector<uint32_t> len;
-    if (n) {
+    std::vector<uint32_t> which;  // requests in digest-row order (empty = all, identity)
+    std::vector<uint64_t> fp;
+    std::vector<uint32_t> tent;
+    std::vector<uint64_t> rl;
+    uint32_t heads = 0;
+    if (dedup) {
+        if (int rc = slice_args(c, slice_ptr, slice_len, slice_first, n, out)) return rc;
+        rl.resize(n);
+        fp.resize(n);
+        tent.resize(n);
+        std::vector<uint8_t> err(n);
+        if (!mirsha::host::dedup_candidates_checked(slice_ptr, slice_len, slice_first, n, slice_first[n],
+                                                    MIRSHA_MAX_MESSAGE_BYTES, rl.data(), err.data(), fp.data(),
+                                                    tent.data(), &heads))
+            return slice_errors(c, err.data(), n);
+        len.assign(rl.begin(), rl.end());
+    } else if (n) {
         if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     }
     c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
@@ -1294,24 +1331,8 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
     if (sl.busy)
         if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
-    // Which requests reach the GPU: all, or one per distinct content.  With
-    // dedup the fingerprint heads (every one of them a final representative)
-    // are packed and queued first; the byte-for-byte confirmation of the
-    // duplicates then runs on the host while the GPU hashes the heads, and
-    // representatives found only there (fingerprint collisions, rare) follow
-    // in a second launch.
-    const bool dedup = (flags & MIRSHA_SUBMIT_DEDUP) && n > 1;
-    std::vector<uint32_t> which;  // requests in digest-row order (empty = all, identity)
-    std::vector<uint64_t> fp;
-    std::vector<uint32_t> tent;
-    std::vector<uint64_t> rl;
     sl.rank.clear();
     if (dedup) {
-        rl.assign(len.begin(), len.end());
-        fp.resize(n);
-        tent.resize(n);
-        const uint32_t heads = mirsha::host::dedup_candidates(slice_ptr, slice_len, slice_first, n, rl.data(),
-                                                              fp.data(), tent.data());
         which.reserve(heads);
         for (uint32_t i = 0; i < n; i++)
             if (tent[i] == i) which.push_back(i);

@@ -287,15 +287,9 @@ bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, u
     }
 }
 
-uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                          const uint64_t* req_len, uint64_t* fp, uint32_t* tent) {
-    if (n == 0) return 0;
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; i++) total += req_len[i];
-    parallel_for(n, threads_for(total, n), [&](uint32_t lo, uint32_t hi) {
-        for (uint32_t i = lo; i < hi; i++) fp[i] = fingerprint(ptr, len, first[i], first[i + 1]);
-    });
-    // Tentative representative: first request with the same (fingerprint, length).
+namespace {
+// Tentative representative: first request with the same (fingerprint, length).
+uint32_t assign_heads(uint32_t n, const uint64_t* req_len, const uint64_t* fp, uint32_t* tent) {
     std::unordered_map<uint64_t, uint32_t> head;
     head.reserve((size_t)n * 2);
     uint32_t heads = 0;
@@ -306,6 +300,62 @@ uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const 
         heads += tent[i] == i;
     }
     return heads;
+}
+}  // namespace
+
+bool dedup_candidates_checked(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                              uint32_t ns, uint64_t max_len, uint64_t* req_len, uint8_t* err, uint64_t* fp,
+                              uint32_t* tent, uint32_t* heads) {
+    *heads = 0;
+    if (n == 0) return true;
+    const bool weak = weak_fp();
+    std::atomic<bool> bad{false};
+    parallel_for(n, threads_for(16ull * ns, n), [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; i++) {
+            err[i] = 0;
+            req_len[i] = 0;
+            fp[i] = 0;
+            if (first[i + 1] < first[i] || first[i + 1] > ns) { err[i] = 1; bad = true; continue; }
+            Fp f;
+            bool over = false;  // past max_len: no more bytes read (as slice_lengths, which reads none)
+            for (uint32_t s = first[i]; s < first[i + 1]; s++) {
+                const uint64_t L = len[s];
+                const uint8_t* p = ptr[s];
+                if (L && !p) { err[i] = 2; break; }
+                if (!over && f.total + L > max_len) over = true;
+                if (weak || over) { f.total += L; continue; }
+                if (f.nc == 0 && L == 8) {  // as fingerprint(): whole words at a word boundary
+                    uint64_t w;
+                    memcpy(&w, p, 8);
+                    f.total += 8;
+                    f.word(w);
+                } else if (f.nc == 0 && L == 32 && (f.idx & 3u) == 0) {
+                    f.total += 32;
+                    f.words4(p);
+                } else if (L) {
+                    f.bytes(p, L);
+                }
+            }
+            if (!err[i] && f.total > max_len) err[i] = 3;
+            if (err[i]) { bad = true; continue; }
+            req_len[i] = f.total;
+            fp[i] = weak ? 0 : f.final();
+        }
+    });
+    if (bad) return false;
+    *heads = assign_heads(n, req_len, fp, tent);
+    return true;
+}
+
+uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                          const uint64_t* req_len, uint64_t* fp, uint32_t* tent) {
+    if (n == 0) return 0;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) total += req_len[i];
+    parallel_for(n, threads_for(total, n), [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t i = lo; i < hi; i++) fp[i] = fingerprint(ptr, len, first[i], first[i + 1]);
+    });
+    return assign_heads(n, req_len, fp, tent);
 }
 
 uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,

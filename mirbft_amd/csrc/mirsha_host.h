@@ -47,6 +47,15 @@ uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32
 uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
                           const uint64_t* req_len, uint64_t* fp, uint32_t* tent);
 
+// dedup_candidates with the call's slice validation folded into the same walk
+// over the slice arrays (config 4: 15.7 M slices of 8-32 B, so the arrays are
+// as large as the payload): per request its length req_len[i] and err[i]
+// (0 ok, 1 slice_first not monotone or past ns, 2 a NULL slice with bytes,
+// 3 longer than max_len).  Returns false (tent unset) if any err[i] != 0.
+bool dedup_candidates_checked(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                              uint32_t ns, uint64_t max_len, uint64_t* req_len, uint8_t* err, uint64_t* fp,
+                              uint32_t* tent, uint32_t* heads);
+
 // Second half: confirms every tentative match byte for byte and resolves
 // fingerprint collisions; fills rep[] as dedup_plan.  Returns distinct count.
 uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,

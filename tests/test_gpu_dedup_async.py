@@ -230,3 +230,35 @@ def test_dedup_collision_path_second_launch():
     env = dict(os.environ, MIRSHA_DEDUP_WEAK_FP="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("case", ["null_slice", "not_monotone", "too_long"])
+def test_slice_argument_errors_dedup_and_plain(engine, case):
+    """Invalid slice arrays are rejected the same way by the dedup call (whose
+    validation rides in its fingerprint walk) and the plain one: same code,
+    same first offending request, no byte read past a too-long request's
+    limit (its slice is a 16-byte buffer declared 4 GiB long), and the
+    context still hashes afterwards."""
+    from mirbft_amd import SliceArrays
+    from mirbft_amd._lib import MirshaError
+
+    keep = [np.frombuffer(bytes(range(16)), dtype=np.uint8).copy() for _ in range(6)]
+    ptr = np.array([k.ctypes.data for k in keep], dtype=np.uint64)
+    ln = np.full(6, 16, dtype=np.uint64)
+    first = np.array([0, 2, 4, 6], dtype=np.uint32)
+    want_code, bad = _lib.MIRSHA_EINVAL, 1
+    if case == "null_slice":
+        ptr[3] = 0
+    elif case == "not_monotone":
+        first = np.array([0, 4, 2, 6], dtype=np.uint32)
+    else:
+        ln[3] = 1 << 32
+        want_code = _lib.MIRSHA_ERANGE
+    sl = SliceArrays(ptr, ln, first, keep)
+    for dedup in (True, False):
+        with pytest.raises(MirshaError) as e:
+            engine.hash_slice_arrays(sl, dedup=dedup)
+        assert e.value.code == want_code
+        assert f"request {bad}" in str(e.value), str(e.value)
+    ok = [[b"abc", b"def"], [b"abcdef"], [b"xyz"]]
+    assert rows(engine.hash_slices(ok, dedup=True)) == want(ok)
