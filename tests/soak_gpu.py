@@ -1,0 +1,181 @@
+#!/usr/bin/env python3
+"""Randomised GPU soak (run by hand / tools/gpu scripts, not collected by
+pytest): for a time budget, random shapes through every entry point --
+host arenas with gaps and odd alignments, sliced requests with duplicates
+(plain and dedup), async submit / wait in shuffled order, request -> list
+digests (nulls, empty and shared lists) through the host call and through
+device plans in every mode, tile-queue count and list-tile form, overlapped
+cycles -- each checked bit for bit against the oracle (test infrastructure,
+oracle/).  Prints a progress line every ~15 s; exits 1 at the first mismatch
+with the seed that reproduces it.
+
+Usage: python tests/soak_gpu.py [--seconds 120] [--seed 1]"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+import oracle_py  # noqa: E402
+from mirbft_amd import Engine  # noqa: E402
+from mirbft_amd import _lib  # noqa: E402
+
+EDGE = [0, 1, 15, 16, 17, 55, 56, 63, 64, 65, 119, 120, 127, 128, 183, 184, 247, 248, 272, 4112]
+
+
+def lengths(rng, n):
+    kind = rng.integers(0, 4)
+    if kind == 0:  # one length (uniform tiles, tail form)
+        return np.full(n, int(rng.choice(EDGE + [int(rng.integers(0, 400))])), dtype=np.uint32)
+    if kind == 1:  # block-boundary mix
+        return rng.choice(EDGE, n).astype(np.uint32)
+    if kind == 2:  # small uniform random
+        return rng.integers(0, 600, n).astype(np.uint32)
+    ln = rng.integers(0, 300, n).astype(np.uint32)  # a few long messages
+    ln[rng.random(n) < 0.01] = rng.integers(1000, 70000)
+    return ln
+
+
+def arena_for(rng, ln):
+    """Messages at random gaps (some overlapping) from a random base alignment."""
+    n = ln.size
+    gaps = rng.integers(0, 9, n).astype(np.uint64) if rng.random() < 0.5 else np.zeros(n, np.uint64)
+    off = np.zeros(n, dtype=np.uint64)
+    pos = np.uint64(rng.integers(0, 4))
+    for i in range(n):
+        off[i] = pos
+        pos += np.uint64(ln[i]) + gaps[i]
+        if rng.random() < 0.02 and ln[i] > 8:  # overlap the next message with this one
+            pos -= np.uint64(4)
+    end = int((off + ln.astype(np.uint64)).max()) if n else 0
+    arena = rng.integers(0, 256, max(end, int(pos)) + 1, dtype=np.uint8)
+    return arena, off
+
+
+def lists_for(rng, n, n_lists):
+    sizes = rng.integers(0, int(rng.choice([4, 21, 60, 501])), n_lists)
+    sizes[rng.random(n_lists) < 0.1] = 0
+    idx = rng.integers(0, max(n, 1), int(sizes.sum())).astype(np.uint32)
+    idx[rng.random(idx.size) < 0.05] = _lib.MIRSHA_NULL_INDEX
+    first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    return idx, first
+
+
+def check(ok, what, seed):
+    if not ok:
+        print(f"MISMATCH: {what} (seed {seed})", flush=True)
+        sys.exit(1)
+
+
+def case_host(eng, rng, seed):
+    n = int(rng.integers(1, 6000))
+    ln = lengths(rng, n)
+    arena, off = arena_for(rng, ln)
+    want = oracle_py.hash_requests(arena, off, ln)
+    check(np.array_equal(eng.hash_batch(arena, off, ln), want), f"hash_batch n={n}", seed)
+    idx, first = lists_for(rng, n, int(rng.integers(0, 400)))
+    req, bat = eng.hash_requests_then_batches(arena, off, ln, idx, first)
+    check(np.array_equal(req, want), "requests_then_batches: requests", seed)
+    check(np.array_equal(bat, oracle_py.batch_digests(want, idx, first)), "requests_then_batches: lists", seed)
+
+
+def case_slices(eng, rng, seed):
+    n = int(rng.integers(1, 800))
+    pool = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in lengths(rng, max(n // 4, 1))]
+    reqs = []
+    for _ in range(n):
+        b = pool[int(rng.integers(0, len(pool)))]
+        cuts = sorted(int(x) for x in rng.integers(0, len(b) + 1, int(rng.integers(0, 6))))
+        parts, last = [], 0
+        for c in cuts + [len(b)]:
+            parts.append(b[last:c])
+            last = c
+        reqs.append(parts)
+    want = oracle_py.hash_messages([b"".join(r) for r in reqs])
+    dedup = bool(rng.random() < 0.5)
+    check(np.array_equal(eng.hash_slices(reqs, dedup=dedup), want), f"hash_slices dedup={dedup} n={n}", seed)
+    # async: several submissions, waited in a shuffled order
+    batches = [reqs[i::3] for i in range(3)]
+    tickets = [eng.submit_slices(b, dedup=bool(rng.random() < 0.5)) for b in batches]
+    for k in rng.permutation(3):
+        got = eng.wait(tickets[k])
+        check(np.array_equal(got, want[k::3]), "submit/wait", seed)
+
+
+def case_plan(eng, rng, seed):
+    n = int(rng.integers(1, 20000))
+    ln = lengths(rng, n)
+    ln = np.minimum(ln, 5000).astype(np.uint32)
+    arena, off = arena_for(rng, ln)
+    idx, first = lists_for(rng, n, int(rng.integers(1, 1500)))
+    mode = str(rng.choice(["auto", "fused", "sequential"]))
+    os.environ["MIRSHA_FUSED_PACE"] = str(int(rng.integers(1, 5)))
+    os.environ["MIRSHA_FUSED_LIST_TILES"] = str(int(rng.integers(0, 3)))
+    plan = eng.pipeline(n, idx, first, ln, mode=mode)
+    os.environ.pop("MIRSHA_FUSED_PACE")
+    os.environ.pop("MIRSHA_FUSED_LIST_TILES")
+    want = oracle_py.hash_requests(arena, off, ln)
+    want_l = oracle_py.batch_digests(want, idx, first)
+    d_arena = torch.from_numpy(arena).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(ln.view(np.int32)).cuda()
+    nl = first.size - 1
+    d_req = [torch.zeros((n, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_lst = torch.zeros((max(nl, 1), 32), dtype=torch.uint8, device="cuda")
+    args = (d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr())
+    for _ in range(int(rng.integers(1, 4))):
+        d_req[0].zero_()
+        d_lst.zero_()
+        torch.cuda.synchronize()  # torch's stream vs the engine's own (non-blocking) stream
+        eng.hash_requests_then_batches_device(plan, *args, d_req[0].data_ptr(), d_lst.data_ptr())
+        plan.status()
+        check(np.array_equal(d_req[0].cpu().numpy(), want), f"plan {mode}: requests n={n}", seed)
+        check(np.array_equal(d_lst.cpu().numpy()[:nl], want_l), f"plan {mode}: lists ({nl})", seed)
+    if plan.mode_name in ("fused", "sequential") and rng.random() < 0.5:  # overlapped cycles + flush
+        for i in range(3):
+            prev = d_req[(i + 1) % 2].data_ptr() if i else 0
+            d_lst.zero_()
+            torch.cuda.synchronize()
+            if i < 2:
+                eng.pipeline_overlap_device(plan, *args, d_req[i % 2].data_ptr(), prev, d_lst.data_ptr())
+            else:
+                eng.pipeline_overlap_device(plan, 0, 0, 0, 0, 0, prev, d_lst.data_ptr())
+            eng.sync()
+            if i < 2:
+                check(np.array_equal(d_req[i % 2].cpu().numpy(), want), f"overlap {mode}: requests", seed)
+            if i:
+                check(np.array_equal(d_lst.cpu().numpy()[:nl], want_l), f"overlap {mode}: lists", seed)
+        plan.status()
+    plan.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=120.0)
+    ap.add_argument("--seed", type=int, default=1)
+    a = ap.parse_args()
+    eng = Engine(0)
+    t0 = last = time.time()
+    counts = {"host": 0, "slices": 0, "plan": 0}
+    k = 0
+    while time.time() - t0 < a.seconds:
+        seed = a.seed * 1_000_003 + k
+        rng = np.random.default_rng(seed)
+        which = ("host", "slices", "plan")[k % 3]
+        {"host": case_host, "slices": case_slices, "plan": case_plan}[which](eng, rng, seed)
+        counts[which] += 1
+        k += 1
+        if time.time() - last > 15:
+            print(f"{time.time() - t0:.0f} s: {counts}", flush=True)
+            last = time.time()
+    eng.close()
+    print(f"soak ok: {k} cases in {time.time() - t0:.0f} s {counts}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -429,6 +429,7 @@ def _plan_run(engine, plan, arena, off, lens, n_lists, runs=2):
     for _ in range(runs):
         d_req.zero_()
         d_lst.zero_()
+        torch.cuda.synchronize()  # torch's stream vs the engine's own (non-blocking) stream
         engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), arena.size, d_off.data_ptr(),
                                                  d_len.data_ptr(), d_req.data_ptr(), d_lst.data_ptr())
         plan.status()
@@ -463,6 +464,7 @@ def test_pipeline_device_full_size(engine, mode, cfg, data_len, n, bs):
     for _ in range(2):
         d_req.zero_()
         d_bat.zero_()
+        torch.cuda.synchronize()  # torch's stream vs the engine's own (non-blocking) stream
         engine.hash_requests_then_batches_device(plan, d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(),
                                                  d_len.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
         plan.status()
@@ -635,16 +637,18 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
     for _ in range(2):
         d_req[0].zero_()
         d_bat.zero_()
+        torch.cuda.synchronize()  # torch's stream vs the engine's own (non-blocking) stream
         engine.hash_requests_then_batches_device(plan, *args, d_req[0].data_ptr(), d_bat.data_ptr())
         plan.status()
         assert np.array_equal(d_req[0].cpu().numpy(), want_req)
         assert np.array_equal(d_bat.cpu().numpy(), want_bat)
     for i in range(3):  # two cycles of the same stream, then the flush
         d_bat.zero_()
-        torch.cuda.synchronize()
         prev = d_req[(i + 1) % 2].data_ptr() if i else 0
         if i < 2:
             d_req[i % 2].zero_()
+        torch.cuda.synchronize()  # torch's stream vs the engine's own (non-blocking) stream
+        if i < 2:
             engine.pipeline_overlap_device(plan, *args, d_req[i % 2].data_ptr(), prev, d_bat.data_ptr())
         else:
             engine.pipeline_overlap_device(plan, 0, 0, 0, 0, 0, prev, d_bat.data_ptr())
@@ -711,6 +715,7 @@ def test_config5_generator_and_wide_arena(engine):
     d_out = torch.empty((n, 32), dtype=torch.uint8, device="cuda")
     for d_order in (None, torch.from_numpy(order.view(np.int32)).cuda()):
         d_out.zero_()
+        torch.cuda.synchronize()  # torch's stream vs the engine's own (non-blocking) stream
         engine.hash_batch_device(d_arena.data_ptr(), arena_len, d_off.data_ptr(), d_len.data_ptr(),
                                  None if d_order is None else d_order.data_ptr(), n, d_out.data_ptr())
         engine.sync()
