@@ -5,7 +5,7 @@ host arenas with gaps and odd alignments, sliced requests with duplicates
 (plain and dedup), async submit / wait in shuffled order, request -> list
 digests (nulls, empty and shared lists) through the host call and through
 device plans in every mode, tile-queue count and list-tile form, overlapped
-cycles -- each checked bit for bit against the oracle (test infrastructure,
+cycles, launches of 65K-400K requests -- each checked bit for bit against the oracle (test infrastructure,
 oracle/).  Prints a progress line every ~15 s; exits 1 at the first mismatch
 with the seed that reproduces it.
 
@@ -154,6 +154,45 @@ def case_plan(eng, rng, seed):
     plan.close()
 
 
+def case_large(eng, rng, seed):
+    """Launches past 1,024 tiles (the LDS request kernel at full occupancy,
+    the uniform-tile and tail forms, bucketed orders) on device buffers."""
+    n = int(rng.integers(65_537, 400_000))
+    kind = rng.integers(0, 3)
+    if kind == 0:
+        ln = np.full(n, int(rng.choice(EDGE[1:] + [int(rng.integers(1, 700))])), dtype=np.uint32)
+    elif kind == 1:
+        ln = rng.choice(EDGE, n).astype(np.uint32)
+    else:
+        ln = rng.integers(0, 700, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(ln[:-1].astype(np.uint64), out=off[1:])
+    off += np.uint64(rng.integers(0, 4))
+    arena = rng.integers(0, 256, int(off[-1]) + int(ln[-1]) + 1, dtype=np.uint8)
+    want = oracle_py.hash_requests(arena, off, ln, threads=8)
+    d_arena = torch.from_numpy(arena).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(ln.view(np.int32)).cuda()
+    d_out = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    eng.hash_batch_device(d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(), None, n,
+                          d_out.data_ptr())
+    eng.sync()
+    check(np.array_equal(d_out.cpu().numpy(), want), f"large hash_batch_device n={n} kind={kind}", seed)
+    idx, first = lists_for(rng, n, int(rng.integers(1, 3000)))
+    plan = eng.pipeline(n, idx, first, ln, mode=str(rng.choice(["auto", "fused", "sequential"])))
+    d_lst = torch.zeros((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    d_out.zero_()
+    torch.cuda.synchronize()
+    eng.hash_requests_then_batches_device(plan, d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr(),
+                                          d_out.data_ptr(), d_lst.data_ptr())
+    plan.status()
+    check(np.array_equal(d_out.cpu().numpy(), want), f"large plan {plan.mode_name}: requests n={n}", seed)
+    check(np.array_equal(d_lst.cpu().numpy(), oracle_py.batch_digests(want, idx, first)),
+          f"large plan {plan.mode_name}: lists", seed)
+    plan.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
@@ -161,13 +200,13 @@ def main():
     a = ap.parse_args()
     eng = Engine(0)
     t0 = last = time.time()
-    counts = {"host": 0, "slices": 0, "plan": 0}
+    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0}
     k = 0
     while time.time() - t0 < a.seconds:
         seed = a.seed * 1_000_003 + k
         rng = np.random.default_rng(seed)
-        which = ("host", "slices", "plan")[k % 3]
-        {"host": case_host, "slices": case_slices, "plan": case_plan}[which](eng, rng, seed)
+        which = ("host", "slices", "plan", "host", "slices", "plan", "large")[k % 7]
+        {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large}[which](eng, rng, seed)
         counts[which] += 1
         k += 1
         if time.time() - last > 15:
