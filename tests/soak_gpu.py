@@ -5,7 +5,7 @@ host arenas with gaps and odd alignments, sliced requests with duplicates
 (plain and dedup), async submit / wait in shuffled order, request -> list
 digests (nulls, empty and shared lists) through the host call and through
 device plans in every mode, tile-queue count and list-tile form, overlapped
-cycles, launches of 65K-400K requests -- each checked bit for bit against the oracle (test infrastructure,
+cycles, launches of 65K-400K requests, checkpoint chains -- each checked bit for bit against the oracle (test infrastructure,
 oracle/).  Prints a progress line every ~15 s; exits 1 at the first mismatch
 with the seed that reproduces it.
 
@@ -193,6 +193,38 @@ def case_large(eng, rng, seed):
     plan.close()
 
 
+def case_chains(eng, rng, seed):
+    """Streaming checkpoint chains (mirsha_chains_*) against hashlib streaming
+    hashers: uniform and skewed writes (one chain taking most digests), sums of
+    repeated / random ids, resets."""
+    import hashlib
+
+    from mirbft_amd import CheckpointChains
+
+    n = int(rng.integers(1, 3000))
+    ch = CheckpointChains(eng, n)
+    ref = [hashlib.sha256() for _ in range(n)]
+    for cycle in range(int(rng.integers(1, 8))):
+        m = int(rng.integers(0, 5000))
+        digests = rng.integers(0, 256, (m, 32), dtype=np.uint8)
+        if rng.random() < 0.3:  # skewed: one hot chain
+            chain_of = np.where(rng.random(m) < 0.9, int(rng.integers(0, n)), rng.integers(0, n, m)).astype(np.uint32)
+        else:
+            chain_of = rng.integers(0, n, m).astype(np.uint32)
+        ch.write(digests, chain_of)
+        for d, c in zip(digests, chain_of):
+            ref[c].update(d.tobytes())
+        cp = rng.integers(0, n, int(rng.integers(0, 40))).astype(np.uint32)
+        got = ch.sum(cp)
+        check([g.tobytes() for g in got] == [ref[c].digest() for c in cp], f"chains n={n} cycle {cycle}", seed)
+        if rng.random() < 0.5:
+            cp = np.unique(cp)
+            ch.reset(cp)
+            for c in cp:
+                ref[c] = hashlib.sha256()
+    ch.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
@@ -200,13 +232,14 @@ def main():
     a = ap.parse_args()
     eng = Engine(0)
     t0 = last = time.time()
-    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0}
+    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0, "chains": 0}
     k = 0
     while time.time() - t0 < a.seconds:
         seed = a.seed * 1_000_003 + k
         rng = np.random.default_rng(seed)
-        which = ("host", "slices", "plan", "host", "slices", "plan", "large")[k % 7]
-        {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large}[which](eng, rng, seed)
+        which = ("host", "slices", "plan", "host", "slices", "plan", "large", "chains")[k % 8]
+        {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large,
+         "chains": case_chains}[which](eng, rng, seed)
         counts[which] += 1
         k += 1
         if time.time() - last > 15:
