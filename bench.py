@@ -254,15 +254,16 @@ class BatchWorkload:
         n_o, ms_o = self.eng.kernel_time(KERNEL_OVERLAP)
         if n_o:
             # One launch: this cycle's request compressions + the previous cycle's batch chains.
-            hbm = self.n * self.stride + self.n * 32 + int(self.first[-1]) * 32 + self.nbat * 32
+            hbm = self.n * (self.stride + 32 + 12) + int(self.first[-1]) * 32 + self.nbat * 32
             return "sha256_msgs_overlap_kernel", n_o, ms_o, self.req_blocks + self.bat_blocks, hbm
         n_f, ms_f = self.eng.kernel_time(KERNEL_FUSED)
         if n_f:
             # One launch does the request AND the batch compressions.
-            hbm = self.n * self.stride + self.n * 32 + int(self.first[-1]) * 32 + self.nbat * 32
+            hbm = self.n * (self.stride + 32 + 12) + int(self.first[-1]) * 32 + self.nbat * 32
             return "sha256_fused_paced_kernel", n_f, ms_f, self.req_blocks + self.bat_blocks, hbm
         n_m, ms_m = self.eng.kernel_time(KERNEL_MSGS)
-        return "sha256_msgs_kernel", n_m, ms_m, self.req_blocks, self.n * self.stride + self.n * 32
+        # message bytes + digest + its off (u64) and len (u32) entries
+        return "sha256_msgs_kernel", n_m, ms_m, self.req_blocks, self.n * (self.stride + 32 + 12)
 
     def batch_ms(self):
         return self.eng.kernel_time(KERNEL_LISTS)[1] + self.eng.kernel_time(KERNEL_CHAIN)[1]
