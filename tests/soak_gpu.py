@@ -68,8 +68,7 @@ def lists_for(rng, n, n_lists):
 
 def check(ok, what, seed):
     if not ok:
-        print(f"MISMATCH: {what} (seed {seed})", flush=True)
-        sys.exit(1)
+        raise AssertionError(f"MISMATCH: {what} (seed {seed})")
 
 
 def case_host(eng, rng, seed):
@@ -238,8 +237,12 @@ def main():
         seed = a.seed * 1_000_003 + k
         rng = np.random.default_rng(seed)
         which = ("host", "slices", "plan", "host", "slices", "plan", "large", "chains")[k % 8]
-        {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large,
-         "chains": case_chains}[which](eng, rng, seed)
+        try:
+            {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large,
+             "chains": case_chains}[which](eng, rng, seed)
+        except AssertionError as e:
+            print(e, flush=True)
+            sys.exit(1)
         counts[which] += 1
         k += 1
         if time.time() - last > 15:
