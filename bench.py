@@ -74,7 +74,7 @@ def parse():
     p.add_argument("--config", type=int, default=2, choices=[1] + sorted(CONFIGS),
                    help="BASELINE config (1 = small-cycle latency of the host API)")
     p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
-    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6],
+    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6, 10, 11],
                    help="0 = LDS-staged loader (latency forms for small launches), 1 = direct per-lane loads, "
                         "4 = low-occupancy kernel, 5 = LDS kernel only, 6 = pair kernel")
     p.add_argument("--windows", action="store_true",
@@ -441,7 +441,7 @@ class BatchWorkload:
         mode = self.plan.mode_name if self.plan is not None else "none"
         if self.overlap:
             return {"batch_pass": "overlapped: the previous cycle's batch chains in each cycle's request launch"}
-        return {"batch_kernel_avg_ms": self.batch_ms() / self.a.steps,
+        return {"batch_kernel_avg_ms": getattr(self, "batch_ms_timed", 0.0) / self.a.steps,
                 "batch_pass": {"none": "sequential batch kernel (plain device API)",
                                "fused": "fused into the request launch (readiness counters, no second kernel)",
                                "sequential": "plan: request kernel then batch kernel"}[mode],
@@ -807,6 +807,10 @@ def main():
         # line's extras); the value and the roofline come from the pass above.
         eng.set_timing_mask(range(32))
         timed(True)
+    # Batch-pass kernel time of the last timing pass, read before
+    # overlap_cycles() resets the engine's timers.
+    if hasattr(wl, "batch_ms"):
+        wl.batch_ms_timed = wl.batch_ms()
 
     # Configs 2/3 with a sequential plan: the overlapped-cycles figure, right
     # behind the timed region too (the chip still at its load clock).
@@ -820,6 +824,7 @@ def main():
         ghz, cyc = eng.clock_probe(a.probe_iters)
         probe = {"clock_ghz": ghz, "cycles_per_wave_compression": cyc}
 
+    dt_rank = dt
     if dist:
         t = torch.tensor([dt], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -855,6 +860,20 @@ def main():
 
     cpu = wl.cpu_baseline(a.cpu_seconds) if rank == 0 and world == 1 and a.cpu_seconds > 0 else None
 
+    # Per-rank evidence (control plane, after the timed region): which device
+    # each rank ran on and its own dominant-kernel time, so a multi-GPU line
+    # shows N distinct GPUs each near the single-GPU kernel rate.
+    props = torch.cuda.get_device_properties(dev)
+    rank_info = {"rank": rank, "local_rank": local, "device": local,
+                 "device_uuid": str(getattr(props, "uuid", "")), "pci_bus_id": getattr(props, "pci_bus_id", None),
+                 "digests": int(wl.digests), "wall_ms_per_step": dt_rank / a.steps * 1e3,
+                 "kernel": kname, "kernel_avg_launch_ms": ms_k / max(n_k, 1),
+                 "frac": achieved_tops / VALU_PEAK_TOPS}
+    per_rank = [rank_info]
+    if dist:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, rank_info)
+
     if rank == 0:
         line = {
             "metric": "SHA-256 digests/s (request + batch digests), Actions.Hash stream",
@@ -873,7 +892,7 @@ def main():
                 "workload": f"config{a.config}: {wl.desc}",
                 **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair"}[a.variant],
+                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair", 10: "cu", 11: "cu_noyield"}[a.variant],
             },
             "gb_per_s_hashed": gbps,
             "roofline": {
@@ -905,6 +924,10 @@ def main():
             "events_in_timed_loop": bool(a.events_in_timed_loop),
             "timed_kernels": a.timed_kernels,
             "self_check": check_ok,
+            "per_rank": per_rank,
+            "distributed": {"world_size": world, "backend": backend if dist else None,
+                            "data_path_collectives": "none: each rank hashes its own request range; "
+                                                     "barriers and max / sum reductions of timings only"},
             "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
         }

@@ -78,8 +78,13 @@ void* mirsha_ctx_stream(mirsha_ctx* ctx);
  *     SIMDs -- and one of at most 1024 groups (one wave per SIMD) the
  *     low-occupancy kernel: prefetching direct loads, no-yield rounds;
  *     MIRSHA_PAIR=0 in the environment disables the pair forms),
+ *     A launch of 1,025..4,096 groups (at most 4 per SIMD) takes the CU-block
+ *     kernel: one workgroup of 4k waves per CU, exactly k waves per SIMD,
+ *     next-block chunks prefetched into registers.
  * 1 = direct per-lane loads, 4 = the low-occupancy kernel at any size,
- * 5 = the LDS kernel at any size, 6 = the pair kernel at any size.
+ * 5 = the LDS kernel at any size, 6 = the pair kernel at any size,
+ * 10 = the CU-block kernel at any size (groups beyond 4 per SIMD run in
+ *     later workgroups, one CU at a time).
  * All are bit-exact.  2, 3, 7, 8 (round-1 A/B forms) are retired: EINVAL. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
@@ -189,7 +194,9 @@ int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
 #define MIRSHA_PROF_DEVICE 3
 #define MIRSHA_PROF_SCATTER 4
 #define MIRSHA_PROF_TOTAL 5
-#define MIRSHA_PROF_PHASES 6
+/* not a time: H2D chunks of the last synchronous call (0 = single-shot staging) */
+#define MIRSHA_PROF_CHUNKS 6
+#define MIRSHA_PROF_PHASES 7
 int mirsha_ctx_host_profile(const mirsha_ctx* ctx, double* ms_out, int n);
 
 /* Request digests, then the dependent batch digests computed ON DEVICE from
@@ -267,9 +274,18 @@ void mirsha_pipeline_destroy(mirsha_pipeline* p);
 int mirsha_pipeline_mode(const mirsha_pipeline* p);
 /* Synchronises the context stream and reports a fused run whose readiness
  * watchdog expired (MIRSHA_EHIP; never expected, the launch is deadlock-free
- * by construction).  MIRSHA_OK otherwise. */
+ * by construction).  MIRSHA_OK otherwise.
+ * Fail closed: a list pair whose wait expired stores no digest of its lists
+ * (d_batch_out keeps its old bytes there) and sets the plan's sticky error
+ * word (host-mapped memory); from then on every run on the plan
+ * (mirsha_hash_requests_then_batches_device, mirsha_pipeline_overlap_device)
+ * returns MIRSHA_EHIP without launching, and so does this call.  The device
+ * calls are asynchronous: a run's own expiry is reported by the next call on
+ * the plan or by this call after it.  Destroy the plan and create a new one.
+ * (MIRSHA_AB=1 MIRSHA_TEST_FUSED_WATCHDOG=<ticks of 100 MHz> at plan creation
+ * shortens the 2 s watchdog; tests only.) */
 int mirsha_pipeline_status(mirsha_ctx* ctx, mirsha_pipeline* p);
-/* Diagnostics of a fused plan created with MIRSHA_FUSED_TRACE=1 in the
+/* Diagnostics of a fused plan created with MIRSHA_AB=1 MIRSHA_FUSED_TRACE=1 in the
  * environment: the last run's timeline (s_memrealtime ticks, 100 MHz) --
  * per tile [start, end, info] at [3t, 3t+1, 3t+2] (info = HW_ID | XCC_ID << 32
  * | queue << 40 | slot << 44), per readiness chunk the time its list wave

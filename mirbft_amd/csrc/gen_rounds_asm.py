@@ -30,7 +30,7 @@ filler gives nearly the same (5,041), two fillers or `s_nop 1` lose, and a
 filler after the 2-cycle-class ops loses.
 
 Run:  python gen_rounds_asm.py > sha256_rounds_asm.h
-      python gen_rounds_asm.py --ab > ../../tools/sha256_rounds_asm_ab.h
+      python gen_rounds_asm.py --ab > ../../tools/sha256_rounds_asm_ab.h   (tools only, not tracked)
 """
 
 K = [
@@ -320,11 +320,16 @@ TAIL_SCALARS = ["kw4", "kw14", "kw15", "c4", "c14", "c15", "cs16", "cs17", "cs19
 
 def emit_fn_tail(name, normal_variant):
     ch, ad, km, nops = VARIANTS[normal_variant]
-    out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16], const TailWords& k) {{",
+    out = ["template <class H = NoHook>",
+           f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16], const TailWords& k, H hook = {{}}) {{",
            "    uint32_t t0, t1, t2, t3; uint32_t kt;"]
+    stmt = 0
     import re
     defined = {f"w{i}" for i in range(4)}  # window words 4..15 are first WRITTEN (W20..W31)
     for j0, j1 in TAIL_STATEMENTS:
+        if stmt:
+            out.append(f"    hook({stmt - 1});")
+        stmt += 1
         body = []
         for j in range(j0, j1):
             body += tail_round(j)
@@ -353,6 +358,8 @@ def emit_fn_tail(name, normal_variant):
         out.append(f"        : {', '.join(ins)});")
     # rounds 32..63: the ordinary statements (every window word is live)
     for j0 in range(32, 64, 8):
+        out.append(f"    hook({stmt - 1});")
+        stmt += 1
         body = block(j0, ch, ad, km, nops)
         out.append(f"    // rounds {j0}..{j0 + 7}")
         out.append("    asm volatile(")
@@ -412,9 +419,12 @@ AB_VARIANTS = {
 
 
 def emit_fn(name, ch_mode, add_mode, k_mode, nops, rounds=(0, 64)):
-    out = [f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16]) {{",
+    out = ["template <class H = NoHook>",
+           f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16], H hook = {{}}) {{",
            "    uint32_t t0, t1, t2, t3;" + (" uint32_t kt;" if k_mode == "smov" else "")]
     for j0 in range(rounds[0], rounds[1], 8):
+        if j0 != rounds[0]:
+            out.append(f"    hook({(j0 - rounds[0]) // 8 - 1});")
         body = block(j0, ch_mode, add_mode, k_mode, nops)
         out.append(f"    // rounds {j0}..{j0 + 7}")
         out.append("    asm volatile(")
@@ -452,6 +462,13 @@ def emit():
         "",
         "// s[0..7] = working variables a..h (updated in place: after 8 rounds the",
         "// names have rotated back), w[0..15] = schedule window (consumed).",
+        "// hook(k) runs between asm statements k and k + 1 (k = 0, 1, ...): a caller",
+        "// interleaves other work (e.g. staging the next block) with the rounds.",
+        "struct NoHook {",
+        "    __device__ __forceinline__ void operator()(int) const {}",
+        "};",
+        "#define MIRSHA_NOHOOK_DEFINED",
+        "",
     ]
     for name, (ch, ad, km, nops) in VARIANTS.items():
         out += emit_fn(name, ch, ad, km, nops)
@@ -481,6 +498,12 @@ def emit_ab():
         "#include <stdint.h>",
         "",
         "namespace mirsha {",
+        "",
+        "#ifndef MIRSHA_NOHOOK_DEFINED",
+        "struct NoHook {",
+        "    __device__ __forceinline__ void operator()(int) const {}",
+        "};",
+        "#endif",
         "",
     ]
     for name, (ch, ad, km, nops) in AB_VARIANTS.items():

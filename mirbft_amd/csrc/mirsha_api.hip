@@ -158,6 +158,12 @@ struct mirsha_pipeline {
     uint32_t q_first[mirsha::kFusedMaxQueues + 1] = {};  // tile queues (fused_build)
     uint64_t epoch = 0;  // completed runs of a fused plan
     DevBuf d_tadj_first, d_tadj, d_cbase, d_expected, d_counters, d_ctl, d_trace;
+    // Sticky error word of a fused plan, in host-mapped memory: the launch's
+    // list waves set it on a readiness-watchdog expiry; every later call on the
+    // plan reads it without a synchronisation and fails (fail closed).
+    unsigned long long* h_err = nullptr;
+    unsigned long long* d_err = nullptr;
+    unsigned long long watchdog = mirsha::kFusedWatchdogTicks;
     bool trace = false;
     std::vector<uint32_t> cidx, cfirst;      // compacted lists (no null entries)
     std::vector<uint32_t> order;             // request processing order
@@ -310,9 +316,9 @@ struct ArenaSrc {
     uint64_t total = 0;
 };
 
-// A boolean knob from the environment ("1" = set), read once per call site.
+// A boolean A/B or diagnostic knob ("1" = set; only with MIRSHA_AB=1).
 bool getenv_flag(const char* name) {
-    const char* e = getenv(name);
+    const char* e = mirsha::ab_getenv(name);
     return e && e[0] == '1';
 }
 
@@ -691,6 +697,7 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     c->prof[MIRSHA_PROF_PACK] = t_pack;
     c->prof[MIRSHA_PROF_DEVICE] = t_wait;
     c->prof[MIRSHA_PROF_SCATTER] = t_out;
+    c->prof[MIRSHA_PROF_CHUNKS] = nch;
     return MIRSHA_OK;
 }
 
@@ -731,6 +738,7 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
     // request bytes, plan = metadata block, device = queue -> sync, scatter =
     // digests to the caller.  (validate is filled by the caller.)
     auto t0 = Clock::now();
+    c->prof[MIRSHA_PROF_CHUNKS] = 0;  // single-shot staging
     const uint32_t entries = n_lists ? first[n_lists] : 0u;
     const bool inl = src.total <= kInlineArena;
     // Large arenas first: their chunks DMA while the metadata is built.
@@ -1052,7 +1060,7 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
     const uint32_t cus = (uint32_t)prop.multiProcessorCount;
     p->pace = kFusedDefaultPace;
-    if (const char* e = getenv("MIRSHA_FUSED_PACE"))
+    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_PACE"))
         p->pace = std::min<uint32_t>(mirsha::kPacedMaxPace, std::max<uint32_t>(1u, (uint32_t)atoi(e)));
     // one list pair per group, up to kFusedMaxListBlocks CUs (more groups: each pair takes several)
     p->list_blocks = std::min<uint32_t>(std::min<uint32_t>(p->n_groups, kFusedMaxListBlocks), cus / 8u);
@@ -1060,7 +1068,7 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     // config 3's 4,096 tiles otherwise leave 144 as a fifth tile on the 988
     // SIMDs of the tile blocks.
     p->list_tiles = kFusedDefaultListTiles;
-    if (const char* e = getenv("MIRSHA_FUSED_LIST_TILES")) p->list_tiles = std::min<uint32_t>(2u, (uint32_t)atoi(e));
+    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_LIST_TILES")) p->list_tiles = std::min<uint32_t>(2u, (uint32_t)atoi(e));
     if (p->list_blocks == 0) p->list_tiles = 0;
     const uint32_t LB = p->list_blocks, P = p->pace;
     // tile waves of one list block per slot s (pair: slot 0 on SIMDs 0 and 1)
@@ -1102,8 +1110,21 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     HIP_TRY(c, p->d_ctl.ensure(8ull * mirsha::kCtlWords));
     HIP_TRY(c, hipMemsetAsync(p->d_ctl.p, 0, 8ull * mirsha::kCtlWords, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (!p->h_err) {
+        void* h = nullptr;
+        HIP_TRY(c, hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        p->h_err = static_cast<unsigned long long*>(h);
+        void* d = nullptr;
+        HIP_TRY(c, hipHostGetDevicePointer(&d, h, 0));
+        p->d_err = static_cast<unsigned long long*>(d);
+    }
+    *reinterpret_cast<volatile unsigned long long*>(p->h_err) = 0ull;
+    // Test-only (MIRSHA_AB=1): the readiness watchdog in 100 MHz ticks, e.g. 0
+    // to force the fail-closed path (tests/test_gpu_parity.py).
+    p->watchdog = mirsha::kFusedWatchdogTicks;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_TEST_FUSED_WATCHDOG")) p->watchdog = strtoull(e, nullptr, 10);
     p->epoch = 0;
-    const char* tr = getenv("MIRSHA_FUSED_TRACE");
+    const char* tr = mirsha::ab_getenv("MIRSHA_FUSED_TRACE");
     p->trace = tr && atoi(tr) != 0;
     if (p->trace) {
         const size_t words = 3ull * p->n_tiles + 2ull * p->n_counters + p->n_groups;
@@ -1111,6 +1132,16 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
         HIP_TRY(c, hipMemsetAsync(p->d_trace.p, 0, 8ull * std::max<size_t>(words, 1), c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
+    return MIRSHA_OK;
+}
+
+// The plan's sticky error word, read without a synchronisation: set by an
+// earlier run's expired readiness wait, whose list digests were not written.
+int fused_failed(mirsha_ctx* c, const mirsha_pipeline* p) {
+    if (p->h_err && *reinterpret_cast<const volatile unsigned long long*>(p->h_err))
+        return fail(c, MIRSHA_EHIP,
+                    "fused pass: a list wave's readiness wait expired (watchdog); its list digests were not "
+                    "written and the plan refuses further runs");
     return MIRSHA_OK;
 }
 
@@ -1122,6 +1153,7 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
               const uint32_t* d_len, uint8_t* d_req_out, uint8_t* d_list_out, bool overlap = false,
               const uint8_t* overlap_prev = nullptr) {
     if (p->n_tiles + p->n_groups == 0) return MIRSHA_OK;
+    if (int rc = fused_failed(c, p)) return rc;
     mirsha::FusedArgs a{};
     a.arena = d_arena;
     a.off = d_off;
@@ -1137,6 +1169,8 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.expected = p->d_expected.as<uint32_t>();
     a.counters = p->d_counters.as<unsigned long long>();
     a.ctl = p->d_ctl.as<unsigned long long>();
+    a.err = p->d_err;
+    a.watchdog = p->watchdog;
     a.trace = p->trace ? p->d_trace.as<unsigned long long>() : nullptr;
     a.n_counters = p->n_counters;
     for (uint32_t q = 0; q <= mirsha::kFusedMaxQueues; q++) a.q_first[q] = p->q_first[std::min(q, p->pace)];
@@ -1160,12 +1194,8 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
 
 int fused_status(mirsha_ctx* c, mirsha_pipeline* p) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (p->mode != MIRSHA_PIPELINE_FUSED || !p->d_ctl.p) return MIRSHA_OK;
-    unsigned long long e = 0;
-    HIP_TRY(c, hipMemcpyAsync(&e, p->d_ctl.as<unsigned long long>() + mirsha::kCtlError, 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (e) return fail(c, MIRSHA_EHIP, "fused pass: a list wave's readiness wait expired (watchdog)");
-    return MIRSHA_OK;
+    if (p->mode != MIRSHA_PIPELINE_FUSED) return MIRSHA_OK;
+    return fused_failed(c, p);
 }
 
 // AUTO: the fused launch pays when a few LONG chains would otherwise run after
@@ -1216,6 +1246,8 @@ void pipeline_free(mirsha_pipeline* p) {
     p->d_counters.release();
     p->d_ctl.release();
     p->d_trace.release();
+    if (p->h_err) (void)hipHostFree(p->h_err);
+    p->h_err = p->d_err = nullptr;
 }
 
 
@@ -1806,6 +1838,7 @@ int mirsha_pipeline_overlap_device(mirsha_ctx* c, mirsha_pipeline* p, const uint
             return fused_run(c, p, d_arena, arena_len, d_off, d_len, d_req_out, chains ? d_prev_batch_out : nullptr,
                              true, chains ? d_prev_req : nullptr);
         if (!chains) return MIRSHA_OK;
+        if (int rc = fused_failed(c, p)) return rc;
         return timed_launch(c, 1, [&] {  // flush: the last cycle's chains alone, producer/consumer pairs
             return mirsha::launch_chain_pair(d_prev_req, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
                                              p->d_cfirst.as<uint32_t>(), p->n_lists, d_prev_batch_out, c->stream);
@@ -1831,7 +1864,7 @@ int mirsha_pipeline_overlap_device(mirsha_ctx* c, mirsha_pipeline* p, const uint
     a.n_lists = p->n_lists;
     a.list_out = d_prev_batch_out;
     a.list_waves = chains ? (p->n_lists + 63u) / 64u : 0u;
-    if (const char* e = getenv("MIRSHA_OVERLAP_CHAIN_PRIO")) a.chain_prio = (uint32_t)atoi(e) & 3u;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_OVERLAP_CHAIN_PRIO")) a.chain_prio = (uint32_t)atoi(e) & 3u;
     return timed_launch(c, 5, [&] { return mirsha::launch_msgs_overlap(a, c->stream); });
 }
 
@@ -2039,8 +2072,11 @@ int mirsha_clock_probe(mirsha_ctx* c, uint32_t iters, double* clock_ghz, double*
     if (int rc = use_device(c)) return rc;
     hipDeviceProp_t prop;
     HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
-    // One 256-thread workgroup = one wave per SIMD of a CU; kProbeWavesPerSimd per CU.
-    const uint32_t blocks = (uint32_t)prop.multiProcessorCount * mirsha::kProbeWavesPerSimd;
+    // One 256-thread workgroup = one wave per SIMD of a CU; kProbeWavesPerSimd per CU
+    // (MIRSHA_AB=1 MIRSHA_PROBE_WAVES=k: k per SIMD, occupancy A/B).
+    uint32_t wps = mirsha::kProbeWavesPerSimd;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_PROBE_WAVES")) wps = std::min(8u, std::max(1u, (uint32_t)atoi(e)));
+    const uint32_t blocks = (uint32_t)prop.multiProcessorCount * wps;
     const uint32_t waves = 4u * blocks;
     DevBuf stamps, sink;
     HIP_TRY(c, stamps.ensure(24ull * waves));
@@ -2070,7 +2106,7 @@ int mirsha_clock_probe(mirsha_ctx* c, uint32_t iters, double* clock_ghz, double*
     *clock_ghz = ghz[waves / 2];
     // Span in shader cycles at that clock, per SIMD, per wave-compression.
     const double span_cycles = (double)(last - first) * 10.0 * *clock_ghz;
-    *cycles_per_wave_compression = span_cycles / ((double)iters * mirsha::kProbeWavesPerSimd);
+    *cycles_per_wave_compression = span_cycles / ((double)iters * wps);
     return MIRSHA_OK;
 }
 

@@ -31,8 +31,10 @@ int env_threads() {
 
 bool weak_fp() {
     static const bool v = [] {
+        // test-only (with MIRSHA_AB=1): every fingerprint equal
+        const char* ab = getenv("MIRSHA_AB");
         const char* e = getenv("MIRSHA_DEDUP_WEAK_FP");
-        return e && e[0] == '1';
+        return ab && ab[0] == '1' && e && e[0] == '1';
     }();
     return v;
 }
@@ -202,18 +204,7 @@ void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, ui
         fn(0, n);
         return;
     }
-#ifdef MIRSHA_AB_SPAWN_THREADS  // A/B build only: round-1 form, threads spawned per call
-    std::vector<std::thread> ts;
-    const uint32_t step = (n + threads - 1) / threads;
-    for (int t = 1; t < threads; t++) {
-        const uint32_t lo = std::min<uint64_t>((uint64_t)t * step, n), hi = std::min<uint64_t>((uint64_t)(t + 1) * step, n);
-        if (lo < hi) ts.emplace_back([&fn, lo, hi] { fn(lo, hi); });
-    }
-    fn(0, std::min(step, n));
-    for (auto& th : ts) th.join();
-#else
     pool().run(n, threads, fn);
-#endif
 }
 
 uint64_t fingerprint(const uint8_t* const* ptr, const uint64_t* len, uint32_t s0, uint32_t s1) {

@@ -20,10 +20,17 @@ enum : int {
     kVariantLowOcc = 4,
     kVariantLdsOnly = 5,
     kVariantPair = 6,
+    kVariantCu = 10,      // CU-block form (one workgroup per CU, prefetching; at most 4 tiles per SIMD)
 };
 inline bool variant_valid(int v) {
-    return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair;
+    return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair ||
+           v == kVariantCu || v == 11;
 }
+constexpr uint32_t kCuMaxWavesPerSimd = 4;
+uint32_t cu_count();
+// Schedule A/B and diagnostic knobs are read from the environment only when
+// MIRSHA_AB=1 is set too (never in production; none changes a digest).
+const char* ab_getenv(const char* name);
 constexpr uint32_t kLowOccTiles = 1024;   // 256 CUs x 4 SIMDs
 // Small launches take a latency form: at most pair_max_groups() 64-message
 // groups (default kPairMaxGroups: <= 2 pairs per CU, every wave alone on a
@@ -89,8 +96,10 @@ constexpr uint32_t kFusedChunkBlocks = 2;  // list blocks (4 digests) per readin
 // SIMD, at issue priority prio_of(q) (earliest-needed tiles win issue).
 constexpr uint32_t kFusedMaxQueues = 4;
 // ctl words (u64, one 128-B line each): tile tickets at kCtlTileTicket + 16 q,
-// error flag, retired-wave count (the launch's last wave resets the tickets)
-constexpr uint32_t kCtlTileTicket = 0, kCtlError = 64, kCtlDone = 80, kCtlWords = 96;
+// retired-wave count (the launch's last wave resets the tickets)
+constexpr uint32_t kCtlTileTicket = 0, kCtlDone = 80, kCtlWords = 96;
+// Readiness-wait watchdog of the fused launch's list waves (100 MHz ticks): 2 s.
+constexpr unsigned long long kFusedWatchdogTicks = 200000000ull;
 struct FusedArgs {
     const uint8_t* arena;
     const uint64_t* off;
@@ -105,7 +114,9 @@ struct FusedArgs {
     const uint32_t* cbase;       // n_groups + 1: first counter of each list group
     const uint32_t* expected;    // tiles feeding each counter
     unsigned long long* counters;
-    unsigned long long* ctl;     // kCtlWords: tickets + error flag, one 128-B line each
+    unsigned long long* ctl;     // kCtlWords: tickets + retire count, one 128-B line each
+    unsigned long long* err;     // the plan's sticky error word (host-mapped), set on a watchdog expiry
+    unsigned long long watchdog; // readiness-wait limit, 100 MHz ticks (kFusedWatchdogTicks)
     // Optional timeline (s_memrealtime, 100 MHz), NULL = off: per tile [start, end,
     // info] at [3t, 3t+1, 3t+2] (info = HW_ID | XCC_ID << 32 | queue << 40 | slot << 44);
     // per readiness chunk the time its list wave passed the wait at

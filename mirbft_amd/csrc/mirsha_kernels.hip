@@ -43,21 +43,8 @@ __device__ __forceinline__ uint32_t wave_reduce(uint32_t v) {
     const uint32_t r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
     return op(op(r0, r1), op(r2, r3));
 }
-#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 shuffle reductions
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) { const uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64); v = v > o ? v : o; }
-    return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) { const uint32_t o = (uint32_t)__shfl_xor((int)v, s, 64); v = v < o ? v : o; }
-    return __builtin_amdgcn_readfirstlane(v);
-}
-#else
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) { return wave_reduce<true>(v); }
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) { return wave_reduce<false>(v); }
-#endif
 
 // Raw 20 bytes (5 dwords) covering the 16-byte chunk q of block blk of a
 // message at arena offset o: aligned down to 4 bytes, the byte shift is
@@ -214,39 +201,6 @@ __device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uin
         ors, 32u * msg + 16u, 0, kSc1);
 }
 
-#ifdef MIRSHA_AB_STAMPS
-// Diagnostic build only (tools/ab_build.sh stamps): per request tile of the
-// LDS loader, the 100 MHz time at wave start / metadata ready / first block
-// staged / end,
-// and the wave's HW_ID and XCC_ID, for tools/stamp_run.py.  No output
-// depends on them.
-constexpr uint32_t kStampWords = 6, kStampTiles = 1u << 16;
-__device__ unsigned long long g_stamps[kStampWords * kStampTiles];
-#define MIRSHA_STAMP(t, i)                                                               \
-    do {                                                                                 \
-        const unsigned long long _v = __builtin_amdgcn_s_memrealtime();                 \
-        if (lane == 0u && (t) < kStampTiles) g_stamps[kStampWords * (t) + (i)] = _v;      \
-    } while (0)
-#define MIRSHA_STAMP_END(t)                                                              \
-    do {                                                                                 \
-        MIRSHA_STAMP(t, 3);                                                              \
-        unsigned _hw, _xcc;                                                              \
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(_hw));                \
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(_xcc));              \
-        if (lane == 0u && (t) < kStampTiles) {                                           \
-            g_stamps[kStampWords * (t) + 4] = _hw;                                       \
-            g_stamps[kStampWords * (t) + 5] = _xcc;                                      \
-        }                                                                                \
-    } while (0)
-#else
-#define MIRSHA_STAMP(t, i) \
-    do {                   \
-    } while (0)
-#define MIRSHA_STAMP_END(t) \
-    do {                    \
-    } while (0)
-#endif
-
 // Issue priority of a request wave, set before each block's rounds: block b
 // runs at max(0, kPrioTop - b), so a wave that is behind wins issue over one
 // that is ahead.  The SIMD's arbiter otherwise runs its waves in age order:
@@ -257,18 +211,13 @@ __device__ unsigned long long g_stamps[kStampWords * kStampTiles];
 // 190.1 us vs 193.8 / 193.3 us with every block at priority 0; tops 1 and 2
 // and a high top for the launch's last generation only were in between or
 // box-dependent.
-#ifndef MIRSHA_PRIO_TOP  // A/B builds override (tools/ab_build.sh)
-#define MIRSHA_PRIO_TOP 3
-#endif
-constexpr uint32_t kPrioTop = MIRSHA_PRIO_TOP;
+constexpr uint32_t kPrioTop = 3;
 __device__ __forceinline__ void progress_prio(uint32_t blk) {
-#ifndef MIRSHA_AB_NOPRIO
     const uint32_t p = blk < kPrioTop ? kPrioTop - blk : 0u;
     if (p >= 3u) __builtin_amdgcn_s_setprio(3);
     else if (p == 2u) __builtin_amdgcn_s_setprio(2);
     else if (p == 1u) __builtin_amdgcn_s_setprio(1);
     else __builtin_amdgcn_s_setprio(0);
-#endif
 }
 
 // One wave hashes the tile of 64 messages at processing positions
@@ -284,9 +233,106 @@ __device__ __forceinline__ void fixed_prio(uint32_t p) {
     else __builtin_amdgcn_s_setprio(0);
 }
 
+// Software-pipelined block loop of a tile (kPf: launches of at most 4 waves
+// per SIMD, which leave a wave 128 VGPRs), for tiles whose messages are all
+// 4-byte aligned and whose loads all stay inside the arena.  Block b+1's
+// words are staged WHILE block b's rounds run, between the round statements
+// (compress_asm_hooked): after rounds 0-7 its raw chunks (loaded one block
+// earlier) are byte-swapped and written to the wave's LDS tile and block b+2's
+// chunks are loaded; after rounds 16-23 the transposed words are read back.
+// So the transpose's LDS round trip and the loads hide behind this wave's own
+// rounds: with 4 waves per SIMD started together (config 3) the waves reach
+// their staging at the same time and the one-at-a-time form left the SIMD
+// short of issuable waves there (643 us per config-3 launch, profiles/r03b).
+template <bool kNoYield>
+__device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc, const uint32_t vo[4],
+                                                    const uint32_t sel[4], uint32_t L, uint32_t min_l, bool uni,
+                                                    bool tail_ok, const TailWords& tw, uint32_t wave_nb,
+                                                    uint32_t loop_nb, uint32_t nb, uint32_t lane, uint4* my,
+                                                    uint32_t st[8]) {
+    const uint32_t q = lane & 3u;
+    uint32_t nx[4][4];  // raw chunks of the next block to stage
+    auto load_raw = [&](uint32_t blk) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], 64u * blk, 0);
+            nx[j][0] = v[0]; nx[j][1] = v[1]; nx[j][2] = v[2]; nx[j][3] = v[3];
+        }
+    };
+    // Words of block blk (raw chunks in nx) into the LDS tile; mixed tiles pad
+    // per chunk here, uniform tiles after the read (pad_block_uniform).
+    auto write_tile = [&](uint32_t blk) {
+        const uint32_t soff = 64u * blk;
+        const bool pad = soff + 64u > min_l;  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            uint32_t wq[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) wq[k] = be_word(k < 3 ? nx[j][k + 1] : 0u, nx[j][k], sel[j]);
+            if (pad && !uni) {
+                const uint32_t Lm = (uint32_t)__shfl((int)L, 16 * j + (int)(lane >> 2), 64);
+                pad_words(soff + 16u * q, Lm, blk + 1u == blocks_for_len(Lm), q, wq);
+            }
+            my[lds_slot(16u * j + (lane >> 2), q)] = make_uint4(wq[0], wq[1], wq[2], wq[3]);
+        }
+        // LDS ops of a wave execute in order; the fences only keep the compiler
+        // from moving the reads above the writes.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto read_tile = [&](uint32_t w[16]) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+            w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto pad_uniform = [&](uint32_t blk, uint32_t w[16]) {
+        if (64u * blk + 64u > min_l && uni) {  // wave-uniform
+            uint32_t wnb;  // opaque copy: no loop peeling to fold the test (see hash_tile)
+            asm volatile("s_mov_b32 %0, %1" : "=s"(wnb) : "s"(wave_nb));
+            pad_block_uniform(w, 64u * blk, min_l, wnb - blk == 1u);
+        }
+    };
+    uint32_t w[16];
+    load_raw(0u);
+    write_tile(0u);
+    if (1u < wave_nb) load_raw(1u);
+    read_tile(w);
+    for (uint32_t blk = 0; blk < loop_nb; blk++) {
+        pad_uniform(blk, w);
+        const bool next = blk + 1u < wave_nb;  // wave-uniform
+        uint32_t wn[16];
+        progress_prio(blk);
+        compress_asm_hooked<kNoYield>(st, w, blk < nb, [&](int k) {
+            if (k == 0 && next) {
+                write_tile(blk + 1u);
+                if (blk + 2u < wave_nb) load_raw(blk + 2u);
+            } else if (k == 2 && next) {
+                read_tile(wn);
+            }
+        });
+#pragma unroll
+        for (int i = 0; i < 16; i++) w[i] = wn[i];
+    }
+    if (tail_ok) {  // final block (<= 16 message bytes), staged during the loop's last block
+        const uint32_t blk = wave_nb - 1u;
+        pad_block_uniform<4>(w, 64u * blk, min_l, false);
+        progress_prio(blk);
+        if (blk < nb) compress_asm_tail(st, w, tw);
+    }
+}
+
 // kFused (sha256_fused_paced_kernel's tile waves): blocks at the fixed
 // priority fprio, digests stored with sc1 for list waves on other CUs.
-template <bool kLds, bool kWide, bool kFused = false>
+// kPf (launches of at most 4 waves per SIMD, which leave 128 VGPRs per wave):
+// the next block's chunks are loaded into registers before this block's
+// rounds, so a wave never waits on memory between compressions.
+template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false>
 __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
@@ -303,20 +349,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     // metadata loads and first block took ~20 us of a ~60-90 us wave life
     // (tools/stamp_run.py).  Same-box A/B (profiles/r02h): 196.4 us per
     // config-2 launch vs 201.9 us without.
-#ifdef MIRSHA_AB_OLDPROLOGUE  // A/B build only: round-1 prologue (conditional loads, default priority)
-    MIRSHA_STAMP(t, 0);
-    const uint32_t slot = t * 64u + lane;
-    const bool valid = slot < n;
-    const uint32_t msg = valid ? (order ? order[slot] : slot) : 0u;
-    const uint32_t L = valid ? len[msg] : 0u;
-    const uint64_t o = valid ? off[msg] : 0u;
-#else
-#ifndef MIRSHA_AB_NOPRIO  // A/B build only: default-priority prologue
     __builtin_amdgcn_s_setprio(3);
-#endif
-    // (after the priority raise: the stamp's own VALU at priority 0 starved
-    // for ~29 us in second-generation waves, profiles/r02m)
-    MIRSHA_STAMP(t, 0);
     const uint32_t slot = t * 64u + lane;
     const bool valid = slot < n;
     // Unconditional loads (n >= 1; an idle lane reads the last message's
@@ -327,7 +360,6 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
     const uint64_t o_ = off[msg];
     const uint32_t L = valid ? L_ : 0u;
     const uint64_t o = valid ? o_ : 0u;
-#endif
     const uint32_t nb = valid ? blocks_for_len(L) : 0u;
     // The tile's longest message, and from it (blocks_for_len is monotone) the
     // wave-uniform block count (SGPR: scalar block-loop tests).
@@ -366,11 +398,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         // Every message of the tile 4-byte aligned (wave-uniform): a chunk's
         // words are its own 16 bytes, byte-swapped, so the fifth dword of the
         // funnel shift is never loaded (4 instead of 8 loads per block).
-#ifdef MIRSHA_AB_NOALIGNED  // A/B build only (tools/ab_build.sh)
-        const bool aligned = false;
-#else
         const bool aligned = __builtin_amdgcn_ballot_w64(valid && (o & 3u) != 0u) == 0;
-#endif
         // Wave-uniform (SGPR), so the padding test below is a scalar branch (as
         // a VGPR compare it became an exec-mask branch with the word assembly
         // duplicated).
@@ -381,19 +409,11 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         // are applied once per lane AFTER the LDS transpose, with the masks
         // computed on the scalar unit (16 VALU per padded block instead of the
         // per-chunk form's ~128 on the loader side).
-#ifdef MIRSHA_AB_PRODUCER_PAD  // A/B build only: loader-side padding for every tile
-        const bool uni = false;
-#else
         const bool uni = max_l == min_l;
-#endif
         // Final-block tail form (compress_asm_tail) for uniform tiles whose
         // final block holds at most 16 message bytes; its scalars up front.
         const int32_t u_last = (int32_t)(min_l - 64u * (wave_nb - 1u));
-#ifdef MIRSHA_AB_NOTAIL  // A/B build only: every block through compress_asm
-        const bool tail_ok = false;
-#else
         const bool tail_ok = uni && u_last <= 16;
-#endif
         const TailWords tw = tail_words(u_last, min_l);
         uint32_t vo[4], sel[4];
 #pragma unroll
@@ -402,18 +422,6 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             vo[j] = a & ~3u;
             sel[j] = be_sel(a & 3u);
         }
-        MIRSHA_STAMP(t, 1);
-#ifdef MIRSHA_AB_PREFETCH  // A/B build only: next block's chunks in registers (6 waves/SIMD)
-        const bool pf = far && aligned;
-        uint32_t nx[4][4];
-        if (pf) {
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], 0, 0);
-                nx[j][0] = v[0]; nx[j][1] = v[1]; nx[j][2] = v[2]; nx[j][3] = v[3];
-            }
-        }
-#endif
         // One block of the tile into w[] (lane = message): loads, big-endian
         // words, per-chunk padding of mixed tiles, the LDS transpose.
         // trim (the tail-form final block): chunks wholly past the tile's
@@ -424,22 +432,6 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             const uint32_t qq = ln & 3u;
             const bool skip = trim && soff + 16u * qq >= min_l;
             RawChunk rc[4];
-#ifdef MIRSHA_AB_PREFETCH
-            if (pf) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    rc[j].v[0] = nx[j][0]; rc[j].v[1] = nx[j][1]; rc[j].v[2] = nx[j][2]; rc[j].v[3] = nx[j][3];
-                    rc[j].v[4] = 0u;
-                }
-                if (blk + 1u < wave_nb) {
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo[j], soff + 64u, 0);
-                        nx[j][0] = v[0]; nx[j][1] = v[1]; nx[j][2] = v[2]; nx[j][3] = v[3];
-                    }
-                }
-            } else
-#endif
             if (far && !trim) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -498,6 +490,13 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         // branch inside it: two round copies joined inside the loop made the
         // register allocator spill (64 VGPRs is the 8-wave budget).
         const uint32_t loop_nb = tail_ok ? wave_nb - 1u : wave_nb;
+        if constexpr (kPf) {
+            if (far && aligned) {
+                hash_tile_pipelined<kNoYield>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb, lane, my,
+                                              st);
+                goto digest;
+            }
+        }
         for (uint32_t blk = 0; blk < loop_nb; blk++) {
             const uint32_t soff = 64u * blk;
             uint32_t w[16];
@@ -514,7 +513,6 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
                 pad_block_uniform(w, soff, min_l, wnb - blk == 1u);
             }
             block_prio(blk);
-            if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm(st, w);
         }
         // Final block of a uniform tile holding at most 16 message bytes
@@ -533,10 +531,8 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             stage(blk, w, ln, true);
             pad_block_uniform<4>(w, 64u * blk, min_l, false);
             block_prio(blk);
-            if (blk == 0u) MIRSHA_STAMP(t, 2);
             if (blk < nb) compress_asm_tail(st, w, tw);
         }
-        MIRSHA_STAMP_END(t);
     } else if constexpr (kLds) {
         // Wide arenas: the same LDS staging with per-chunk 64-bit addresses
         // and activity tests (one launch over > 4 GiB, BASELINE config 5).
@@ -590,6 +586,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
             if (active) compress_asm(st, w);
         }
     }
+digest:
     if (valid) {
         if constexpr (kFused) {
             const __amdgpu_buffer_rsrc_t ors =
@@ -613,18 +610,8 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 // workgroup's waves (one per SIMD) far apart, so 4-wave workgroups left SIMDs
 // below their 8-wave occupancy (tools/stamp_run.py).  8 waves per SIMD bound
 // the register budget to 64 VGPRs (the wide form keeps 6: 80 VGPRs, no spill).
-#ifdef MIRSHA_AB_WG4  // A/B build only (tools/ab_build.sh): 4-wave workgroups
-constexpr uint32_t kMsgWaves = 4;
-#else
 constexpr uint32_t kMsgWaves = 1;
-#endif
-#if defined(MIRSHA_AB_PREFETCH)  // A/B build only: 5 waves/SIMD (up to 96 VGPRs)
-constexpr uint32_t kMsgOcc = 5, kTileSlots = 256;
-#elif defined(MIRSHA_AB_OCC6)  // A/B build only: 6 waves/SIMD
-constexpr uint32_t kMsgOcc = 6, kTileSlots = 416;  // 6.5 KiB LDS per wave: 24 waves per CU
-#else
 constexpr uint32_t kMsgOcc = 8, kTileSlots = 256;
-#endif
 template <bool kLds, bool kWide = false>
 __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_msgs_kernel(
     const uint8_t* __restrict__ arena, uint64_t arena_len, const uint64_t* __restrict__ off,
@@ -636,6 +623,32 @@ __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_ms
     const uint32_t t = blockIdx.x * kMsgWaves + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
     hash_tile<kLds, kWide>(arena, arena_len, off, len, order, n, out, tile[wv], t, lane);
+}
+
+// CU-block form of the request kernel, for launches of 1,025 to 4,096 tiles
+// (at most 4 per SIMD; BASELINE config 3's 2^18 x 4 KB requests are exactly
+// 4,096).  One-wave workgroups leave their placement to the dispatcher, and
+// it stacks them unevenly: config 3's request waves lived 441 us on average
+// in a 653 us launch (SQ_WAVE_CYCLES / SQ_WAVES, profiles/r03a), i.e. some
+// SIMDs ran 5-6 tiles while others idled.  Here each CU gets ONE workgroup of
+// 4k waves (kCuLds of LDS holds it alone on its CU), which the CU deals to
+// its SIMDs in cyclic order: exactly k waves per SIMD.  At k <= 4 a wave may
+// hold 128 VGPRs, so the next block's chunks are prefetched into registers.
+constexpr uint32_t kCuLds = 96u * 1024u;
+template <bool kNoYield>
+__global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* __restrict__ arena,
+                                                                 uint64_t arena_len,
+                                                                 const uint64_t* __restrict__ off,
+                                                                 const uint32_t* __restrict__ len,
+                                                                 const uint32_t* __restrict__ order, uint32_t n,
+                                                                 uint8_t* __restrict__ out) {
+    extern __shared__ uint4 cu_lds[];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * (blockDim.x >> 6) + wv;
+    if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
+    hash_tile<true, false, false, true, kNoYield>(arena, arena_len, off, len, order, n, out, cu_lds + 256u * wv, t,
+                                                  lane);
 }
 
 // ---- overlapped cycles: this cycle's request tiles + the previous cycle's
@@ -1231,17 +1244,24 @@ __device__ __forceinline__ uint64_t poll_counter(const unsigned long long* ctr) 
     return __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load_dwordx2 sc1
 }
 
-// Blocks until *ctr >= target (wave-uniform).  Returns false on watchdog expiry.
+// The plan's sticky error word (host-mapped memory, so every later host call
+// on the plan sees it without a synchronisation): set on any watchdog expiry.
+__device__ __forceinline__ void raise_error(unsigned long long* err) {
+    __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Blocks until *ctr >= target (wave-uniform).  Returns false on watchdog
+// expiry (`watchdog` ticks of the 100 MHz clock; FusedArgs::watchdog).
 __device__ __noinline__ bool wait_counter(const unsigned long long* ctr, uint64_t target,
-                                          unsigned long long* err) {
+                                          unsigned long long* err, uint64_t watchdog) {
     if (target == 0) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (true) {
         const uint64_t v = poll_counter(ctr);
         if (__shfl((int)(v >= target), 0, 64)) return true;
         __builtin_amdgcn_s_sleep(8);  // ~512 cycles between polls
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
-            __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > watchdog) {
+            if (__lane_id() == 0) raise_error(err);
             return false;
         }
     }
@@ -1288,17 +1308,23 @@ __device__ __forceinline__ void load_chunk_digests(__amdgpu_buffer_rsrc_t drs, c
 // that slot and frees it.  LDS flags with workgroup-scope acquire / release
 // (no s_barrier: the list block's other waves have exited); the waits carry
 // the same 2 s watchdog as the readiness waits.
+// Fail closed: a producer whose readiness wait expired sets `aborted` and
+// publishes produced = kRingAbort, so its consumer stops at once and stores
+// no digest of this or any later group (the caller sees the plan's error
+// word: mirsha_pipeline_status and every later call on the plan fail).
 struct FusedPairRing {
     uint4 kw[2][16][64];
     uint32_t produced, consumed;  // blocks handed over / freed, over all groups of the block
+    uint32_t aborted;
 };
+constexpr uint32_t kRingAbort = 0xFFFFFFFFu;
 
 __device__ __forceinline__ bool lds_wait_ge(const uint32_t* p, uint32_t target, unsigned long long* err) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s at 100 MHz
-            __hip_atomic_store(err, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__lane_id() == 0) raise_error(err);
             return false;
         }
     }
@@ -1325,24 +1351,34 @@ struct FusedListShape {
 };
 
 // Consumer side of group g: the rounds of every block from the ring.
-__device__ __forceinline__ void fused_list_consume(const FusedArgs& a, FusedPairRing& ring, uint32_t g,
+// Returns false (no digest stored) once the producer has aborted.
+__device__ __forceinline__ bool fused_list_consume(const FusedArgs& a, FusedPairRing& ring, uint32_t g,
                                                    uint32_t lane, uint32_t& seq) {
     const FusedListShape sh(a, g, lane);
     uint32_t st[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] = kH0[i];
     for (uint32_t blk = 0; blk < sh.wave_nb; blk++, seq++) {
-        if (!lds_wait_ge(&ring.produced, seq + 1u, a.ctl + kCtlError)) return;
+        if (!lds_wait_ge(&ring.produced, seq + 1u, a.err)) return false;
+        if (__hip_atomic_load(&ring.aborted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
         consume_kw(ring.kw[seq & 1u], lane, st, blk < sh.nb);
         lds_publish(&ring.consumed, seq + 1u);
     }
     if (a.trace && lane == 0) a.trace[3u * a.n_tiles + a.n_counters + g] = __builtin_amdgcn_s_memrealtime();
     if (sh.valid) store_digest(a.list_out, sh.k, st);
+    return true;
+}
+
+__device__ __forceinline__ bool fused_abort(FusedPairRing& ring) {
+    __hip_atomic_store(&ring.aborted, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    lds_publish(&ring.produced, kRingAbort);
+    return false;
 }
 
 // Producer side of group g: readiness waits and digest loads a chunk ahead,
-// then each block's schedule + K + W into the ring.
-__device__ __forceinline__ void fused_list_produce(const FusedArgs& a, __amdgpu_buffer_rsrc_t drs,
+// then each block's schedule + K + W into the ring.  Returns false (after
+// fused_abort) when a wait expired: nothing past that point is handed over.
+__device__ __forceinline__ bool fused_list_produce(const FusedArgs& a, __amdgpu_buffer_rsrc_t drs,
                                                    __amdgpu_buffer_rsrc_t irs, FusedPairRing& ring, uint32_t g,
                                                    uint32_t lane, uint32_t& seq) {
     const FusedListShape sh(a, g, lane);
@@ -1353,11 +1389,11 @@ __device__ __forceinline__ void fused_list_produce(const FusedArgs& a, __amdgpu_
     auto stamp = [&](uint32_t at) {
         if (a.trace && lane == 0) a.trace[at] = __builtin_amdgcn_s_memrealtime();
     };
-    if (nchunks == 0) return;
+    if (nchunks == 0) return true;
     uint32_t ixc[kChunkDigests], ixn[kChunkDigests];
     load_chunk_idx(irs, e0, c, 0u, ixc);
     load_chunk_idx(irs, e0, c, 1u, ixn);
-    wait_counter(a.counters + cb, target(0), a.ctl + kCtlError);
+    if (!wait_counter(a.counters + cb, target(0), a.err, a.watchdog)) return fused_abort(ring);
     uint4 dc[2 * kChunkDigests];
     load_chunk_digests(drs, ixc, c, 0u, true, dc);
     uint64_t pollv = 1u < nchunks ? poll_counter(a.counters + cb + 1u) : 0u;
@@ -1396,7 +1432,7 @@ __device__ __forceinline__ void fused_list_produce(const FusedArgs& a, __amdgpu_
                     w[15] = L << 3;
                 }
                 // slot seq & 1 was last filled with block seq - 2: free once seq - 1 blocks are consumed
-                if (seq >= 2u && !lds_wait_ge(&ring.consumed, seq - 1u, a.ctl + kCtlError)) return;
+                if (seq >= 2u && !lds_wait_ge(&ring.consumed, seq - 1u, a.err)) return fused_abort(ring);
                 produce_kw(w, ring.kw[seq & 1u], lane);
                 lds_publish(&ring.produced, seq + 1u);
                 seq++;
@@ -1405,7 +1441,7 @@ __device__ __forceinline__ void fused_list_produce(const FusedArgs& a, __amdgpu_
         stamp(3u * a.n_tiles + a.n_counters + a.n_groups + cb + chunk);
         if (nc < nchunks) {
             if (!have_next) {  // exposed: wait for the next chunk's tiles, then load it
-                wait_counter(a.counters + cb + nc, target(nc), a.ctl + kCtlError);
+                if (!wait_counter(a.counters + cb + nc, target(nc), a.err, a.watchdog)) return fused_abort(ring);
                 load_chunk_digests(drs, ixn, c, nc, true, dn);
                 if (nc + 1u < nchunks) pollv = poll_counter(a.counters + cb + nc + 1u);
             }
@@ -1415,6 +1451,7 @@ __device__ __forceinline__ void fused_list_produce(const FusedArgs& a, __amdgpu_
             for (uint32_t i = 0; i < kChunkDigests; i++) ixn[i] = ixnn[i];
         }
     }
+    return true;
 }
 
 // Block = 4 x pace waves (pace per SIMD; wave w on SIMD w % 4), one block per
@@ -1449,7 +1486,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     FusedPairRing& ring = *reinterpret_cast<FusedPairRing*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedRingOff);
     const bool list_block = blockIdx.x < a.list_waves;  // list_waves carries the number of LIST BLOCKS
     if (threadIdx.x < 4u) simd_waves[threadIdx.x] = 0u;
-    if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = 0u;
+    if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = ring.aborted = 0u;
     __syncthreads();
     uint32_t hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -1467,9 +1504,10 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             const __amdgpu_buffer_rsrc_t irs =
                 __builtin_amdgcn_make_buffer_rsrc((void*)a.cidx, (short)0, (int)(4u * a.n_entries), 0x00020000);
             for (uint32_t g = blockIdx.x; g < a.n_groups; g += a.list_waves)
-                fused_list_produce(a, drs, irs, ring, g, lane, seq);
+                if (!fused_list_produce(a, drs, irs, ring, g, lane, seq)) break;
         } else {
-            for (uint32_t g = blockIdx.x; g < a.n_groups; g += a.list_waves) fused_list_consume(a, ring, g, lane, seq);
+            for (uint32_t g = blockIdx.x; g < a.n_groups; g += a.list_waves)
+                if (!fused_list_consume(a, ring, g, lane, seq)) break;
         }
         tiles = a.list_tiles != 0u;
         own = false;  // chains done: tiles left in the last queue (the overflow)
@@ -1602,13 +1640,6 @@ __global__ __launch_bounds__(256) void clock_probe_kernel(uint32_t iters, unsign
     sink[blockIdx.x * 256u + threadIdx.x] = st[0] ^ st[7];
 }
 
-#ifdef MIRSHA_AB_STAMPS
-extern "C" int mirsha_ab_stamps(unsigned long long* out, uint64_t words) {
-    if (words > (uint64_t)kStampWords * kStampTiles) words = (uint64_t)kStampWords * kStampTiles;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), 8 * words, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
-}
-#endif
-
 hipError_t launch_clock_probe(uint32_t blocks, uint32_t iters, unsigned long long* stamps, uint32_t* sink,
                               hipStream_t s) {
     clock_probe_kernel<<<blocks, 256, 0, s>>>(iters, stamps, sink);
@@ -1616,14 +1647,32 @@ hipError_t launch_clock_probe(uint32_t blocks, uint32_t iters, unsigned long lon
 }
 
 // ---- host-side launchers --------------------------------------------------
+const char* ab_getenv(const char* name) {
+    const char* ab = getenv("MIRSHA_AB");
+    return (ab && ab[0] == '1') ? getenv(name) : nullptr;
+}
+
 uint32_t pair_max_groups() {
     static const uint32_t v = [] {
-        const char* e = getenv("MIRSHA_PAIR");
+        const char* e = ab_getenv("MIRSHA_PAIR");
         if (e && e[0] == '0') return 0u;
-        const char* m = getenv("MIRSHA_PAIR_MAX_GROUPS");
+        const char* m = ab_getenv("MIRSHA_PAIR_MAX_GROUPS");
         return m ? (uint32_t)strtoul(m, nullptr, 10) : kPairMaxGroups;
     }();
     return v;
+}
+
+// Compute units of the current device (cached per device).
+uint32_t cu_count() {
+    static uint32_t cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256u;
+    if (!cached[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        cached[dev] = (uint32_t)v;
+    }
+    return cached[dev];
 }
 
 hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
@@ -1643,6 +1692,27 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
     }
     if (variant == kVariantLowOcc || (variant == kVariantLds && tiles <= kLowOccTiles)) {
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        return hipGetLastError();
+    }
+    if (variant == kVariantCu || variant == 11 || (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
+        // k waves per SIMD, one workgroup of 4k waves per CU
+        const uint32_t k = (tiles + 4u * cu_count() - 1u) / (4u * cu_count());
+        const uint32_t wg_waves = 4u * std::min(k, kCuMaxWavesPerSimd);
+        static bool attr = false;
+        if (!attr) {
+            hipError_t e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<false>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        const uint32_t cgrid = (tiles + wg_waves - 1u) / wg_waves;
+        if (variant == 11)
+            sha256_msgs_cu_kernel<true><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+        else
+            sha256_msgs_cu_kernel<false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantDirect)

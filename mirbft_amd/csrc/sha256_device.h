@@ -8,9 +8,6 @@
 #include <stdint.h>
 
 #include "sha256_rounds_asm.h"
-#if defined(MIRSHA_AB_KSGPR) || defined(MIRSHA_AB_ROUNDS) || defined(MIRSHA_AB_LAT_ROUNDS)  // A/B builds only (tools/ab_build.sh)
-#include "sha256_rounds_asm_ab.h"
-#endif
 
 namespace mirsha {
 
@@ -85,15 +82,27 @@ __device__ __forceinline__ void compress_asm(uint32_t st[8], uint32_t w[16]) {
     uint32_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = st[i];
-#if defined(MIRSHA_AB_KSGPR)
-    rounds_asm_ksgpr(s, w);
-#elif defined(MIRSHA_AB_ROUNDS)  // e.g. -DMIRSHA_AB_ROUNDS=rounds_asm_y_rot
-    MIRSHA_AB_ROUNDS(s, w);
-#else
     rounds_asm(s, w);
-#endif
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] += s[i];
+}
+
+// compress_asm with work interleaved between its asm statements (hook(k)
+// after statement k, see sha256_rounds_asm.h) and the state updated only on
+// lanes with `live` set: every lane runs the rounds (a wave instruction costs
+// the same at any exec mask), so a hook that stages data for the whole wave
+// never runs under a divergent mask.
+template <bool kNoYield = false, class H>
+__device__ __forceinline__ void compress_asm_hooked(uint32_t st[8], uint32_t w[16], bool live, H hook) {
+    uint32_t s[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = st[i];
+    if constexpr (kNoYield)
+        rounds_asm_nonop(s, w, hook);
+    else
+        rounds_asm(s, w, hook);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = live ? st[i] + s[i] : st[i];
 }
 
 // The wave-uniform scalars of a final block whose words 4..15 are all padding
@@ -136,11 +145,7 @@ __device__ __forceinline__ void compress_asm_lat(uint32_t st[8], uint32_t w[16])
     uint32_t s[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) s[i] = st[i];
-#if defined(MIRSHA_AB_LAT_ROUNDS)  // e.g. -DMIRSHA_AB_LAT_ROUNDS=rounds_asm_ilp
-    MIRSHA_AB_LAT_ROUNDS(s, w);
-#else
     rounds_asm_nonop(s, w);
-#endif
 #pragma unroll
     for (int i = 0; i < 8; i++) st[i] += s[i];
 }

@@ -33,7 +33,8 @@ VARIANT_DIRECT = 1
 VARIANT_LOWOCC = 4
 VARIANT_LDS_ONLY = 5
 VARIANT_PAIR = 6
-VARIANTS = (VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR)
+VARIANT_CU = 10
+VARIANTS = (VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR, VARIANT_CU)
 
 
 def _ptr(a: np.ndarray | None) -> int | None:
@@ -365,7 +366,7 @@ class Engine:
         """Config-5 message bytes of requests [first, first + count) at d_arena + d_off[r]."""
         self._check(self._lib.mirsha_synth_mixed_device(self.ctx, seed, first, count, d_off, d_arena))
 
-    HOST_PHASES = ("validate", "plan", "pack", "device", "scatter", "total")
+    HOST_PHASES = ("validate", "plan", "pack", "device", "scatter", "total", "chunks")
 
     def host_profile(self) -> dict:
         """Host-side phases (ms) of the last slice submission (mirsha_ctx_host_profile)."""
@@ -538,6 +539,7 @@ __all__ = [
     "VARIANT_DIRECT",
     "VARIANT_LOWOCC",
     "VARIANT_LDS_ONLY",
+    "VARIANT_CU",
     "VARIANT_PAIR",
     "VARIANTS",
 ]

@@ -113,11 +113,13 @@ def case_plan(eng, rng, seed):
     arena, off = arena_for(rng, ln)
     idx, first = lists_for(rng, n, int(rng.integers(1, 1500)))
     mode = str(rng.choice(["auto", "fused", "sequential"]))
+    os.environ["MIRSHA_AB"] = "1"  # schedule knobs below are read only with MIRSHA_AB=1
     os.environ["MIRSHA_FUSED_PACE"] = str(int(rng.integers(1, 5)))
     os.environ["MIRSHA_FUSED_LIST_TILES"] = str(int(rng.integers(0, 3)))
     plan = eng.pipeline(n, idx, first, ln, mode=mode)
     os.environ.pop("MIRSHA_FUSED_PACE")
     os.environ.pop("MIRSHA_FUSED_LIST_TILES")
+    os.environ.pop("MIRSHA_AB")
     want = oracle_py.hash_requests(arena, off, ln)
     want_l = oracle_py.batch_digests(want, idx, first)
     d_arena = torch.from_numpy(arena).cuda()

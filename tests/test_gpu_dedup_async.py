@@ -227,7 +227,7 @@ def test_dedup_collision_path_second_launch():
         "e.close()\n"
         "print('ok')\n" % (root, os.path.join(root, "tests"))
     )
-    env = dict(os.environ, MIRSHA_DEDUP_WEAK_FP="1")
+    env = dict(os.environ, MIRSHA_AB="1", MIRSHA_DEDUP_WEAK_FP="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 

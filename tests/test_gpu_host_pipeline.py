@@ -20,6 +20,7 @@ from mirbft_amd import SliceArrays, sharding
 pytestmark = pytest.mark.gpu
 
 CHUNK = 32 << 20  # kStageChunk
+PIPE_MAX_LEN = 256 * 64 - 9  # kPipeMaxBlocks: longer messages take the single-shot path
 
 
 def _cfg2(n, data_len=256):
@@ -28,12 +29,20 @@ def _cfg2(n, data_len=256):
     return arena, np.arange(n, dtype=np.uint64) * stride, np.full(n, stride, np.uint32)
 
 
-def _check(eng, arena, off, ln, idx=None, first=None, out=None, batch_out=None):
+def _check(eng, arena, off, ln, idx=None, first=None, out=None, batch_out=None, min_chunks=None):
+    """Digests (and list digests) vs the oracle; min_chunks: the call must
+    have gone through the pipelined path with at least that many H2D chunks
+    (mirsha_ctx_host_profile's chunk count; 0 = single-shot staging)."""
     if idx is None:
         got = eng.hash_batch(arena, off, ln, out=out)
         bat = None
     else:
         got, bat = eng.hash_requests_then_batches(arena, off, ln, idx, first, out=out, batch_out=batch_out)
+    chunks = eng.host_profile()["chunks"]
+    if min_chunks is not None:
+        assert chunks >= min_chunks, f"pipelined path not taken ({chunks} chunks)"
+    else:
+        assert chunks == 0, f"expected single-shot staging, got {chunks} chunks"
     want = oracle_py.hash_requests(np.asarray(arena), off, ln, threads=8)
     assert np.array_equal(got, want)
     if idx is not None:
@@ -63,9 +72,33 @@ def test_config2_full_size_pageable_and_pinned(engine):
                 assert np.array_equal(bat, want_bat)
 
 
-def test_shifted_base_and_straddling_messages(engine):
-    """Messages start at a nonzero arena offset (rebased on the device), and
-    long messages straddle the 32 MiB chunk cuts."""
+def _random_lists(rng, n, n_lists, max_list, null_frac=0.1):
+    sizes = rng.integers(0, max_list, n_lists)
+    idx = rng.integers(0, n, int(sizes.sum())).astype(np.uint32)
+    idx[rng.random(idx.size) < null_frac] = 0xFFFFFFFF
+    return idx, np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+
+
+def test_gapped_arena_pipelined_with_null_lists(engine):
+    """The pipelined path's general in-order layout (kInOrder: gaps between
+    messages, a shifted base, messages straddling every chunk cut, all <= 16 KiB
+    so no message forces the single-shot path): the per-chunk cut search,
+    offsets shipped (no device scan), and random lists with null entries
+    through the lists launch behind the last chunk."""
+    rng = np.random.default_rng(21)
+    lens = rng.integers(0, PIPE_MAX_LEN + 1, 12000).astype(np.uint32)
+    gaps = rng.integers(0, 40, lens.size).astype(np.uint64)
+    off = 777 + np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64) + gaps[:-1])]).astype(np.uint64)
+    arena = rng.integers(0, 256, int(off[-1] + lens[-1]) + 3, dtype=np.uint8)
+    assert arena.size > 2 * CHUNK
+    idx, first = _random_lists(rng, lens.size, 700, 40)
+    _check(engine, arena, off, lens, idx, first, min_chunks=3)
+    _check(engine, arena, off, lens, min_chunks=3)
+
+
+def test_multi_mib_messages_single_shot(engine):
+    """Messages of 5-11 MiB (longer than the pipelined path's per-message
+    limit) at a shifted base take the single-shot staged path."""
     rng = np.random.default_rng(21)
     lens = rng.integers(0, 5000, 30000).astype(np.uint32)
     lens[::997] = rng.integers(5 << 20, 11 << 20, lens[::997].size)  # multi-MiB messages
@@ -77,18 +110,17 @@ def test_shifted_base_and_straddling_messages(engine):
 
 
 def test_mixed_lengths_per_chunk_order_with_lists(engine):
-    """Log-uniform lengths (a bucket order per chunk) plus random lists with
-    null entries over the request digests."""
+    """Log-uniform lengths up to the pipelined limit (a bucket order per chunk,
+    gapless: offsets rebuilt by the device scan) plus random lists with null
+    entries over the request digests, through the pipelined path."""
     rng = np.random.default_rng(22)
-    lens = synth.log_uniform_lengths(synth.SEED_BASE + 22, 20000, 6, 16).astype(np.uint32)
+    lens = synth.log_uniform_lengths(synth.SEED_BASE + 22, 20000, 6, 14).astype(np.uint32)
+    lens = np.minimum(lens, PIPE_MAX_LEN).astype(np.uint32)
     off = np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
     arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
-    assert arena.size > 2 * CHUNK
-    sizes = rng.integers(0, 30, 900)
-    idx = rng.integers(0, lens.size, int(sizes.sum())).astype(np.uint32)
-    idx[rng.random(idx.size) < 0.1] = 0xFFFFFFFF
-    first = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
-    _check(engine, arena, off, lens, idx, first)
+    assert arena.size > CHUNK
+    idx, first = _random_lists(rng, lens.size, 900, 30)
+    _check(engine, arena, off, lens, idx, first, min_chunks=2)
 
 
 def test_out_of_order_dense_arena_single_shot(engine):
@@ -97,15 +129,18 @@ def test_out_of_order_dense_arena_single_shot(engine):
     n = 200000
     arena, off, ln = _cfg2(n)
     perm = np.random.default_rng(23).permutation(n)
-    _check(engine, arena, off[perm], ln[perm])
+    _check(engine, arena, off[perm], ln[perm])  # asserts 0 chunks
 
 
 def test_pipelined_equals_single_shot(engine, monkeypatch):
     n = 300000
     arena, off, ln = _cfg2(n)
     a = engine.hash_batch(arena, off, ln)
+    assert engine.host_profile()["chunks"] >= 2
+    monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_NO_PIPELINED_CALLS", "1")
     b = engine.hash_batch(arena, off, ln)
+    assert engine.host_profile()["chunks"] == 0
     assert np.array_equal(a, b)
     assert np.array_equal(a, oracle_py.hash_requests(arena, off, ln, threads=8))
 
@@ -156,6 +191,7 @@ def test_gapless_shifted_arena_device_offsets(engine, monkeypatch):
     off = 4096 + np.concatenate([[0], np.cumsum(lens[:-1].astype(np.uint64))]).astype(np.uint64)
     arena = rng.integers(0, 256, int(off[-1] + lens[-1]) + 100, dtype=np.uint8)
     assert arena.size > 2 * CHUNK
-    a = _check(engine, arena, off, lens)
+    a = _check(engine, arena, off, lens, min_chunks=2)
+    monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_NO_OFFSET_SCAN", "1")
     assert np.array_equal(engine.hash_batch(arena, off, lens), a)

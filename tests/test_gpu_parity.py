@@ -14,7 +14,7 @@ import synth
 from mirbft_amd import (ActionResults, Actions, Engine, HashRequest, MirshaError, Processor, ProcessorWorkPool,
                         gpu_hasher, hash_batch_multi, hashdata, sharding)
 from mirbft_amd import _lib
-from mirbft_amd.engine import (KERNEL_LISTS, KERNEL_MSGS, VARIANT_DIRECT, VARIANT_LDS, VARIANT_LDS_ONLY,
+from mirbft_amd.engine import (KERNEL_LISTS, KERNEL_MSGS, VARIANT_CU, VARIANT_DIRECT, VARIANT_LDS, VARIANT_LDS_ONLY,
                                VARIANT_LOWOCC, VARIANT_PAIR)
 
 pytestmark = pytest.mark.gpu
@@ -22,8 +22,8 @@ pytestmark = pytest.mark.gpu
 EMPTY = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 
 
-@pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR],
-                ids=["lds", "direct", "lowocc", "lds_only", "pair"])
+@pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR, VARIANT_CU],
+                ids=["lds", "direct", "lowocc", "lds_only", "pair", "cu"])
 def eng(engine, request):
     engine.set_variant(request.param)
     yield engine
@@ -597,6 +597,7 @@ def test_fused_plan_irregular(engine, monkeypatch, pace, list_tiles, seed, n, n_
     """Fused plan (device API) on irregular shapes, three runs on one plan (the
     tile queues' tickets carried across runs), 1-4 tile queues, list blocks
     with and without tile waves."""
+    monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_FUSED_PACE", str(pace))
     monkeypatch.setenv("MIRSHA_FUSED_LIST_TILES", str(list_tiles))
     arena, off, lens, idx, first = _irregular(seed, n, n_lists, max(max_list, 1), max_len)
@@ -618,6 +619,7 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
     whose list blocks also run tile waves (MIRSHA_FUSED_LIST_TILES): two
     ordinary runs, then two overlapped cycles and the flush, bit-exact."""
     torch = _torch()
+    monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_FUSED_LIST_TILES", str(list_tiles))
     n, data_len, bs = 1 << 18, 4096, 500
     stride = 16 + data_len
@@ -661,11 +663,59 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
     plan.close()
 
 
+def test_fused_watchdog_fails_closed(engine, monkeypatch):
+    """A fused run whose readiness waits expire (test-only zero watchdog,
+    MIRSHA_TEST_FUSED_WATCHDOG=0) fails closed: the plan's status is
+    MIRSHA_EHIP, no list digest is written (the output keeps its fill byte),
+    and every later run on the plan is refused without a synchronisation.
+    Request digests are unaffected (tiles never wait).  A new plan with the
+    default watchdog is bit-exact again."""
+    torch = _torch()
+    n, data_len, bs = 20_000, 4096, 500
+    stride = 16 + data_len
+    seed = synth.SEED_BASE + 70
+    idx, first = sharding.batch_lists(n, bs)
+    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    d_req = torch.zeros((n, 32), dtype=torch.uint8, device="cuda")
+    d_bat = torch.full((first.size - 1, 32), 0xA5, dtype=torch.uint8, device="cuda")
+    engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
+    want_req = oracle_py.hash_requests(oracle_py.gen_requests(seed, 0, n, data_len),
+                                       np.arange(n, dtype=np.uint64) * stride, np.full(n, stride), threads=8)
+    args = (d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr())
+    monkeypatch.setenv("MIRSHA_AB", "1")
+    monkeypatch.setenv("MIRSHA_TEST_FUSED_WATCHDOG", "0")
+    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="fused")
+    monkeypatch.delenv("MIRSHA_TEST_FUSED_WATCHDOG")
+    torch.cuda.synchronize()
+    engine.hash_requests_then_batches_device(plan, *args, d_req.data_ptr(), d_bat.data_ptr())
+    with pytest.raises(MirshaError) as e:
+        plan.status()
+    assert e.value.code == _lib.MIRSHA_EHIP
+    assert (d_bat.cpu().numpy() == 0xA5).all(), "a list digest was stored after the watchdog expired"
+    assert np.array_equal(d_req.cpu().numpy(), want_req)
+    with pytest.raises(MirshaError) as e:
+        engine.hash_requests_then_batches_device(plan, *args, d_req.data_ptr(), d_bat.data_ptr())
+    assert e.value.code == _lib.MIRSHA_EHIP
+    with pytest.raises(MirshaError) as e:
+        engine.pipeline_overlap_device(plan, *args, d_req.data_ptr(), d_req.data_ptr(), d_bat.data_ptr())
+    assert e.value.code == _lib.MIRSHA_EHIP
+    plan.close()
+    fresh = engine.pipeline(n, idx, first, np.full(n, stride), mode="fused")
+    torch.cuda.synchronize()
+    engine.hash_requests_then_batches_device(fresh, *args, d_req.data_ptr(), d_bat.data_ptr())
+    fresh.status()
+    assert np.array_equal(d_bat.cpu().numpy(), oracle_py.batch_digests(want_req, idx, first))
+    fresh.close()
+
+
 def test_fused_plans_interleaved(engine, monkeypatch):
     """Two fused plans used alternately: each keeps its own tickets / counters
     (3 and 4 tile queues)."""
     a = _irregular(41, 2000, 200, 40, 400)
     b = _irregular(42, 5000, 90, 300, 200)
+    monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_FUSED_PACE", "3")
     pa = engine.pipeline(a[2].size, a[3], a[4], a[2], mode="fused")
     monkeypatch.setenv("MIRSHA_FUSED_PACE", "4")

@@ -82,7 +82,7 @@ def test_weak_fingerprint_collisions_resolved_exactly():
         "    assert rep.tolist() == want.tolist() and u == wu, seed\n"
         "print('ok')\n" % (ROOT, os.path.join(ROOT, "tests"))
     )
-    env = dict(os.environ, MIRSHA_DEDUP_WEAK_FP="1")
+    env = dict(os.environ, MIRSHA_AB="1", MIRSHA_DEDUP_WEAK_FP="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
 

@@ -20,6 +20,7 @@ OCCUPANCY = {
     "sha256_msgs_kernelILb1ELb1E": 6,      # > 4 GiB arenas (64-bit addressing)
     "sha256_msgs_overlap_kernel": 8,       # overlapped cycles
     "sha256_fused_paced_kernel": 4,        # fused config-3 launch (4 tile waves per SIMD)
+    "sha256_msgs_cu_kernel": 4,            # CU-block request kernel (4 waves per SIMD, prefetching)
     "sha256_chain_kernel": 8,
 }
 

@@ -12,6 +12,8 @@ from __future__ import annotations
 import os
 import random
 import re
+import subprocess
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "mirbft_amd", "csrc", "sha256_rounds_asm.h")
@@ -102,7 +104,7 @@ def run_asm(lines, regs):
 
 
 # ---- header parsing ----------------------------------------------------------
-AB_HDR = os.path.join(ROOT, "tools", "sha256_rounds_asm_ab.h")
+GEN = os.path.join(ROOT, "mirbft_amd", "csrc", "gen_rounds_asm.py")
 
 
 def _functions(path=HDR):
@@ -199,10 +201,13 @@ def test_rounds_kw8_asm_matches_fips():
     assert [env[f"s[{i}]"] for i in range(8)] == ref_rounds(s, w)
 
 
-def test_ab_round_forms_match_fips():
-    """The A/B-only forms (tools/sha256_rounds_asm_ab.h: yield patterns,
-    K-in-SGPR, bfi / add2 / literal variants, the lone-wave ILP order) are
-    bit-identical to FIPS 180-4 too."""
+def test_ab_round_forms_match_fips(tmp_path):
+    """The A/B-only forms (gen_rounds_asm.py --ab, generated for tools/ only:
+    yield patterns, K-in-SGPR, bfi / add2 / literal variants, the lone-wave
+    ILP order) are bit-identical to FIPS 180-4 too."""
+    AB_HDR = str(tmp_path / "sha256_rounds_asm_ab.h")
+    with open(AB_HDR, "w") as f:
+        subprocess.run([sys.executable, GEN, "--ab"], stdout=f, check=True)
     rng = random.Random(4)
     names = [n for n, (sig, _) in _functions(AB_HDR).items() if "uint32_t w[16]" in sig]
     assert "rounds_asm_ilp" in names and len(names) >= 8

@@ -9,6 +9,8 @@ Prints one JSON line per case (kernel ms from HIP events on a private stream).
 """
 import json
 import os
+
+os.environ["MIRSHA_AB"] = "1"  # the library reads the schedule / trace knobs only with MIRSHA_AB=1
 import sys
 
 import numpy as np

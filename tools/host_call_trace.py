@@ -4,7 +4,7 @@ batches) through mirsha_hash_requests_then_batches: per-call wall time, the
 library's host phases, and (MIRSHA_STAGE_TRACE=1, stderr) the per-chunk queue /
 wait / copy-out times of the pipelined path.  Pageable and pinned arenas.
 
-Usage (GPU box):  MIRSHA_STAGE_TRACE=1 python tools/host_call_trace.py [reps]
+Usage (GPU box):  MIRSHA_AB=1 MIRSHA_STAGE_TRACE=1 python tools/host_call_trace.py [reps]
 """
 import json
 import os

@@ -3,6 +3,8 @@
 pass their readiness wait.  Usage: trace_fused.py <config> [pace ...]"""
 import json
 import os
+
+os.environ["MIRSHA_AB"] = "1"  # the library reads the schedule / trace knobs only with MIRSHA_AB=1
 import sys
 
 import numpy as np
