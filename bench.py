@@ -31,6 +31,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -322,6 +323,27 @@ class BatchWorkload:
                 "pinned_arena": {"digests_per_s": self.digests / qdt, "gb_per_s": self.bytes_hashed / qdt / 1e9,
                                  "ms_per_call": qdt * 1e3, "calls_ms": qcalls, "host_phases_ms": qprof,
                                  "note": "the same call on an arena from mirsha_host_alloc (page-locked)"}}
+
+    def cgo_path(self):
+        """The Go binding's HashBatch end to end, slices -> digests
+        (tests/c/cgo_path.c, a separate process with no Python: request
+        Data as 3 heap slices each, packed into the mirsha_host_alloc arena
+        by one or by 16 workers, then mirsha_hash_batch; and the
+        library-packed mirsha_hash_slices).  Config 2 at full size."""
+        exe = os.path.join(ROOT, "tests", "c", "build", "cgo_path")
+        if not os.path.exists(exe):
+            return {"note": f"{exe} not built (__graft_entry__.build())"}
+        r = subprocess.run([exe, str(self.n), str(self.data_len), "16", "5"], capture_output=True, text=True,
+                           timeout=300)
+        if r.returncode != 0:
+            return {"error": r.stderr[-500:]}
+        out = json.loads(r.stdout.splitlines()[-1])
+        out.pop("sample", None)
+        out["note"] = ("INTEGRATION.md GPUHasher.HashBatch made from C: 'serial' = one goroutine packs, "
+                       "'parallel' = 16 goroutines (GOMAXPROCS chunks), 'lib' = mirsha_hash_slices on C slice "
+                       "arrays (library packing overlapped with the DMA); median of 5 calls, digests into pageable "
+                       "memory, PCIe included")
+        return out
 
     def cpu_baseline(self, seconds):
         """Oracle (C port of processor.go:133-143 with SHA-NI compression, the
@@ -761,6 +783,7 @@ def main():
     # PCIe-inclusive host-API rate (rank 0, N=1 only), measured before the
     # device-resident steps.
     pcie = wl.pcie() if rank == 0 and world == 1 and not a.no_pcie else None
+    cgo = wl.cgo_path() if rank == 0 and world == 1 and not a.no_pcie and hasattr(wl, "cgo_path") else None
     torch.cuda.synchronize(dev)
 
     for _ in range(a.warmup):
@@ -929,6 +952,7 @@ def main():
                             "data_path_collectives": "none: each rank hashes its own request range; "
                                                      "barriers and max / sum reductions of timings only"},
             "pcie_inclusive": pcie,
+            "cgo_path": cgo,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -294,6 +294,10 @@ int mirsha_pipeline_status(mirsha_ctx* ctx, mirsha_pipeline* p);
  * [3 n_tiles + n_counters + g].  *words = total length (0 when tracing is off). */
 int mirsha_pipeline_trace(mirsha_ctx* ctx, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words);
 int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t* n_counters, uint32_t* n_groups);
+/* Split tiles of a fused plan: request tiles beyond the launch's tile-wave
+ * slots, each run as *segments_per_tile sequential block-range segments
+ * spread one per SIMD (0, 0 when none). */
+int mirsha_pipeline_split_tiles(const mirsha_pipeline* p, uint32_t* n_split, uint32_t* segments_per_tile);
 /* Device-resident run: request digests to d_req_out (origin order), batch
  * digests to d_batch_out; asynchronous on the context stream. */
 int mirsha_hash_requests_then_batches_device(mirsha_ctx* ctx, mirsha_pipeline* p, const uint8_t* d_arena,

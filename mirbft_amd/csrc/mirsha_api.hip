@@ -164,6 +164,11 @@ struct mirsha_pipeline {
     unsigned long long* h_err = nullptr;
     unsigned long long* d_err = nullptr;
     unsigned long long watchdog = mirsha::kFusedWatchdogTicks;
+    // split tiles (FusedArgs::n_split)
+    uint32_t n_split = 0, seg_per_tile = 0, seg_nominal_nb = 0;
+    std::vector<uint32_t> seg_nb;
+    DevBuf d_seg_nb, d_seg_state, d_seg_flags;
+    uint64_t seg_runs = 0;  // launches of the plan (segment flags are monotone over them)
     bool trace = false;
     std::vector<uint32_t> cidx, cfirst;      // compacted lists (no null entries)
     std::vector<uint32_t> order;             // request processing order
@@ -1088,6 +1093,41 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
         at += 4u * tile_blocks + LB * lb_slot(q);
     }
     p->q_first[P] = p->n_tiles;
+    // Split tiles (FusedArgs::n_split): tiles beyond the tile waves' slots
+    // would run as a fifth tile on some SIMDs (config 3: 72 of 4,096, ending
+    // ~130 us after the rest, profiles/r02af).  Instead each is cut into
+    // block-range segments, one per host SIMD (the last queue's wave of every
+    // tile-block SIMD), so the overflow spreads over the whole grid.
+    p->n_split = p->seg_per_tile = p->seg_nominal_nb = 0;
+    p->seg_nb.clear();
+    const uint32_t hosts = 4u * tile_blocks;
+    if (len && p->n_tiles > p->tile_waves) {
+        const uint32_t ns = p->n_tiles - p->tile_waves;
+        auto tile_blocks_of = [&](uint32_t t) {
+            uint32_t m = 0;
+            for (uint32_t i = 64u * t; i < std::min(n_req, 64u * t + 64u); i++)
+                m = std::max(m, host_blocks(len[p->order[i]]));
+            return m;
+        };
+        // Segment k runs when its host's own tile reaches block k * nom / S:
+        // nom = the median block count of the hosts' own tiles (the last
+        // queue's).  Only a schedule: a host whose own tile is shorter runs
+        // its segment after that tile.
+        std::vector<uint32_t> own;
+        for (uint32_t t = p->q_first[P - 1]; t < p->n_tiles - ns; t++) own.push_back(tile_blocks_of(t));
+        std::vector<uint32_t> snb;
+        for (uint32_t t = p->n_tiles - ns; t < p->n_tiles; t++) snb.push_back(tile_blocks_of(t));
+        const uint32_t smax = *std::max_element(snb.begin(), snb.end());
+        const uint32_t S = std::min(hosts / ns, smax);
+        if (S >= 2 && !own.empty()) {
+            std::nth_element(own.begin(), own.begin() + own.size() / 2, own.end());
+            p->n_split = ns;
+            p->seg_per_tile = S;
+            p->seg_nominal_nb = std::max(1u, own[own.size() / 2]);
+            p->seg_nb = snb;
+            p->q_first[P] = p->n_tiles - ns;
+        }
+    }
     // Device copies.
     auto up = [&](DevBuf& d, const void* h, size_t bytes) -> int {
         HIP_TRY(c, d.ensure(std::max<size_t>(bytes, 4)));
@@ -1109,6 +1149,13 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, p->d_ctl.ensure(8ull * mirsha::kCtlWords));
     HIP_TRY(c, hipMemsetAsync(p->d_ctl.p, 0, 8ull * mirsha::kCtlWords, c->stream));
+    if (p->n_split) {
+        if (int rc = up(p->d_seg_nb, p->seg_nb.data(), sizeof(uint32_t) * p->n_split)) return rc;
+        HIP_TRY(c, p->d_seg_state.ensure(2048ull * p->n_split));
+        HIP_TRY(c, p->d_seg_flags.ensure(128ull * p->n_split));
+        HIP_TRY(c, hipMemsetAsync(p->d_seg_flags.p, 0, 128ull * p->n_split, c->stream));
+    }
+    p->seg_runs = 0;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (!p->h_err) {
         void* h = nullptr;
@@ -1186,9 +1233,19 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.n_tiles = p->n_tiles;
     a.n_groups = (overlap && !overlap_prev) ? 0u : p->n_groups;
     a.list_waves = p->list_blocks;
+    a.n_split = p->n_split;
+    a.seg_per_tile = p->seg_per_tile;
+    a.seg_nominal_nb = p->seg_nominal_nb;
+    a.seg_epoch = p->seg_runs;
+    a.tile_prio_progress = overlap ? 1u : 0u;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_OVERLAP_QUEUE_PRIO")) a.tile_prio_progress = overlap && e[0] != '1';
+    a.seg_nb = p->d_seg_nb.as<uint32_t>();
+    a.seg_state = p->d_seg_state.as<uint32_t>();
+    a.seg_flags = p->d_seg_flags.as<unsigned long long>();
     if (int rc = timed_launch(c, 4, [&] { return mirsha::launch_fused_paced(a, p->grid, p->pace, c->stream); }))
         return rc;
     p->epoch++;
+    p->seg_runs++;
     return MIRSHA_OK;
 }
 
@@ -1246,6 +1303,9 @@ void pipeline_free(mirsha_pipeline* p) {
     p->d_counters.release();
     p->d_ctl.release();
     p->d_trace.release();
+    p->d_seg_nb.release();
+    p->d_seg_state.release();
+    p->d_seg_flags.release();
     if (p->h_err) (void)hipHostFree(p->h_err);
     p->h_err = p->d_err = nullptr;
 }
@@ -1799,6 +1859,13 @@ int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t*
     *n_tiles = p->n_tiles;
     *n_counters = p->n_counters;
     *n_groups = p->n_groups;
+    return MIRSHA_OK;
+}
+
+int mirsha_pipeline_split_tiles(const mirsha_pipeline* p, uint32_t* n_split, uint32_t* segments_per_tile) {
+    if (!p || !n_split || !segments_per_tile) return MIRSHA_EINVAL;
+    *n_split = p->n_split;
+    *segments_per_tile = p->seg_per_tile;
     return MIRSHA_OK;
 }
 

@@ -140,6 +140,24 @@ struct FusedArgs {
     // chunk is ready at epoch x expected; 64-bit so it never wraps.
     unsigned long long epoch;
     uint32_t n_tiles, n_groups, list_waves;
+    // Split tiles: the last n_split tiles in needed-at order (those the tile
+    // waves' slots cannot take, e.g. config 3's 4,096 tiles on 4,024 slots)
+    // run as seg_per_tile sequential block-range segments, segment k of split
+    // tile s hosted by the last queue's wave h = s * seg_per_tile + k of the
+    // tile blocks (h = (block - list blocks) * 4 + SIMD), which runs it when
+    // its own first tile reaches block k * seg_nominal_nb / seg_per_tile.  A
+    // segment's midstate goes through seg_state ([s][8][64] words), its
+    // completion through seg_flags[16 s] (monotone: run seg_epoch, segment k
+    // done at seg_epoch * seg_per_tile + k + 1).  So no SIMD takes a fifth
+    // tile: the overflow spreads as one short segment per SIMD.
+    uint32_t n_split, seg_per_tile, seg_nominal_nb;
+    // Overlapped cycles: tile waves at the request kernel's progress
+    // priorities instead of their queue's (nothing waits on this run's tiles).
+    uint32_t tile_prio_progress;
+    unsigned long long seg_epoch;
+    const uint32_t* seg_nb;            // blocks of each split tile
+    uint32_t* seg_state;
+    unsigned long long* seg_flags;
 };
 // list_waves = number of list BLOCKS (first in the grid); one block per CU
 // (kPacedLds of LDS: 16 waves' 4 KiB staging tiles, then a list block's pair

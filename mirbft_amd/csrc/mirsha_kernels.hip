@@ -226,6 +226,7 @@ __device__ __forceinline__ void progress_prio(uint32_t blk) {
 // 64-bit per-lane addresses for arenas beyond one buffer descriptor.
 // Fixed issue priority of a fused-launch tile wave (its queue's), set before
 // each block's rounds in place of progress_prio.
+constexpr uint32_t kPrioProgress = 4;  // hash_tile<kFused>'s fprio: progress_prio instead of a fixed one
 __device__ __forceinline__ void fixed_prio(uint32_t p) {
     if (p >= 3u) __builtin_amdgcn_s_setprio(3);
     else if (p == 2u) __builtin_amdgcn_s_setprio(2);
@@ -330,18 +331,27 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
 // kFused (sha256_fused_paced_kernel's tile waves): blocks at the fixed
 // priority fprio, digests stored with sc1 for list waves on other CUs.
 // kPf (launches of at most 4 waves per SIMD, which leave 128 VGPRs per wave):
-// the next block's chunks are loaded into registers before this block's
-// rounds, so a wave never waits on memory between compressions.
+// the next block's chunks are staged while this block's rounds run
+// (hash_tile_pipelined).
+// Block range (the fused launch's split tiles, LDS loader only): blocks
+// [b0, b1) of the tile, from the midstate in st (H0 when b0 == 0).  Returns
+// true when the range reached the tile's end: the digest is then stored;
+// otherwise st holds the midstate after block b1 - 1.
 template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false>
-__device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
+__device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
-                                          uint4* my, uint32_t t, uint32_t lane, uint32_t fprio = 0) {
+                                          uint4* my, uint32_t t, uint32_t lane, uint32_t fprio = 0,
+                                          uint32_t b0 = 0u, uint32_t b1 = 0xFFFFFFFFu, uint32_t* st_io = nullptr) {
     auto block_prio = [&](uint32_t blk) {
-        if constexpr (kFused)
-            fixed_prio(fprio);
-        else
+        if constexpr (kFused) {
+            if (fprio == kPrioProgress)
+                progress_prio(blk);
+            else
+                fixed_prio(fprio);
+        } else {
             progress_prio(blk);
+        }
     };
     // Prologue at the highest issue priority, back to 0 at the first
     // compression: a fresh wave is the youngest on its SIMD and at the default
@@ -380,7 +390,8 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
 
     uint32_t st[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) st[i] = kH0[i];
+    for (int i = 0; i < 8; i++) st[i] = (st_io && b0) ? st_io[i] : kH0[i];
+    const bool finished = b1 >= wave_nb;
 
     if constexpr (kLds && !kWide) {
         // Loader roles: this lane fetches quarter q of messages m_j = 16j + lane/4.
@@ -491,13 +502,14 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         // register allocator spill (64 VGPRs is the 8-wave budget).
         const uint32_t loop_nb = tail_ok ? wave_nb - 1u : wave_nb;
         if constexpr (kPf) {
-            if (far && aligned) {
+            if (far && aligned && b0 == 0u && finished) {
                 hash_tile_pipelined<kNoYield>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb, lane, my,
                                               st);
                 goto digest;
             }
         }
-        for (uint32_t blk = 0; blk < loop_nb; blk++) {
+        const uint32_t loop_end = min(loop_nb, b1);
+        for (uint32_t blk = b0; blk < loop_end; blk++) {
             const uint32_t soff = 64u * blk;
             uint32_t w[16];
             stage(blk, w, lane, false);
@@ -520,7 +532,7 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         // 4..15 are padding constants, and the tail rounds take them, and the
         // schedule terms they feed, as scalars (requests of a 16-byte header
         // plus a 2^k-byte payload: BASELINE configs 2 and 3).
-        if (tail_ok) {
+        if (tail_ok && finished) {
             const uint32_t blk = wave_nb - 1u;
             uint32_t w[16];
             // (the lane index through an opaque copy: the LDS slot addresses
@@ -587,6 +599,11 @@ __device__ __forceinline__ void hash_tile(const uint8_t* __restrict__ arena, uin
         }
     }
 digest:
+    if (!finished) {  // a split tile's range: hand the midstate back
+#pragma unroll
+        for (int i = 0; i < 8; i++) st_io[i] = st[i];
+        return false;
+    }
     if (valid) {
         if constexpr (kFused) {
             const __amdgpu_buffer_rsrc_t ors =
@@ -603,6 +620,7 @@ digest:
             store_digest(out, msg, st);
         }
     }
+    return true;
 }
 
 // One wave per workgroup: a workgroup's slot and LDS are released only when
@@ -1454,6 +1472,25 @@ __device__ __forceinline__ bool fused_list_produce(const FusedArgs& a, __amdgpu_
     return true;
 }
 
+// Midstate of split tile s between two segments, [s][word][lane], written
+// through (sc1) and read with sc1 loads by the next segment's host on any
+// XCD after its flag wait (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void store_midstate_sc1(uint32_t* seg_state, uint32_t s, uint32_t lane,
+                                                   const uint32_t st[8]) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(seg_state + 512ull * s), (short)0,
+                                                                        2048, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; i++) __builtin_amdgcn_raw_buffer_store_b32(st[i], rs, 4u * (64u * i + lane), 0, kSc1);
+}
+
+__device__ __forceinline__ void load_midstate_sc1(const uint32_t* seg_state, uint32_t s, uint32_t lane,
+                                                  uint32_t st[8]) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(seg_state + 512ull * s), (short)0,
+                                                                        2048, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4u * (64u * i + lane), 0, kSc1);
+}
+
 // Block = 4 x pace waves (pace per SIMD; wave w on SIMD w % 4), one block per
 // CU (kPacedLds of LDS).  List blocks [0, list_blocks) run a chain pair on
 // SIMDs 0 and 1; their other waves exit at once or, with list_tiles, serve
@@ -1515,30 +1552,111 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     uint4* my = paced_lds + 256u * wv;  // the wave's 4 KiB staging tile
     const uint32_t last = a.n_queues - 1u;
     const uint32_t q = min(slot, last);
-    while (tiles) {
-        const uint32_t qq = own ? q : last;
-        const uint64_t t = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) + a.q_first[qq];
-        if (t >= a.q_first[qq + 1]) {
-            if (own && qq != last) {
-                own = false;
+    // Split tiles (FusedArgs::n_split): this wave hosts segment `seg` if it is
+    // the last queue's wave on a tile-block SIMD with a segment assigned; it
+    // runs the segment when its own first tile reaches block seg_at.
+    constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
+    uint32_t seg = kNoSeg, seg_at = 0u;
+    if (a.n_split && !list_block && slot == last) {
+        const uint32_t h = (blockIdx.x - a.list_waves) * 4u + simd;
+        if (h < a.n_split * a.seg_per_tile) {
+            seg = h;
+            seg_at = (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
+        }
+    }
+    uint64_t t = 0;
+    bool have = false;    // a claimed own tile in progress
+    uint32_t ob0 = 0u;    // its next block
+    uint32_t qq = q;
+    uint32_t st[8];
+    // A host's own tile's midstate while it runs its segment: in the tile
+    // block's unused pair-ring LDS (2 KiB per SIMD's host wave), not registers.
+    uint32_t* own_st = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedRingOff) + 512u * simd;
+    while (true) {
+        if (!have && tiles) {
+            qq = own ? q : last;
+            const uint64_t c = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) + a.q_first[qq];
+            if (c >= a.q_first[qq + 1]) {
+                if (own && qq != last) {
+                    own = false;
+                    continue;
+                }
+                tiles = false;
+            } else {
+                t = c;
+                have = true;
+                ob0 = 0u;
+                if (a.trace && lane == 0) {
+                    uint32_t xcc;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                    a.trace[3 * t] = __builtin_amdgcn_s_memrealtime();
+                    a.trace[3 * t + 2] = (unsigned long long)hw | ((unsigned long long)(xcc & 0xFFu) << 32) |
+                                         ((unsigned long long)qq << 40) | ((unsigned long long)slot << 44);
+                }
+            }
+        }
+        // The next range of work: this wave's segment (at its turn), else its own tile.
+        const bool is_seg = seg != kNoSeg && (!have || ob0 >= seg_at);
+        if (!is_seg && !have) break;
+        uint32_t wt, b0, b1, pr, s_i = 0u, k_i = 0u;
+        if (is_seg) {
+            s_i = seg / a.seg_per_tile;
+            k_i = seg % a.seg_per_tile;
+            const uint32_t S = a.seg_per_tile, nbs = a.seg_nb[s_i];
+            wt = a.n_tiles - a.n_split + s_i;
+            b0 = k_i * nbs / S;
+            b1 = k_i + 1u == S ? 0xFFFFFFFFu : (k_i + 1u) * nbs / S;
+            pr = 3u;  // a segment chain is sequential: run it at the top issue priority
+#pragma unroll
+            for (int i = 0; i < 8; i++) own_st[64 * i + lane] = st[i];
+            // Segment k_i - 1 of this split tile done (this run)?  Fail closed on expiry.
+            // (inline, not wait_counter: a call here spilled the live tile state)
+            bool ok = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0ull;
+            const uint64_t target = a.seg_epoch * S + k_i, t0 = __builtin_amdgcn_s_memrealtime();
+            while (ok && !__shfl((int)(poll_counter(a.seg_flags + 16u * s_i) >= target), 0, 64)) {
+                __builtin_amdgcn_s_sleep(8);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.watchdog) {
+                    if (lane == 0u) raise_error(a.err);
+                    ok = false;
+                }
+            }
+            if (!ok) {  // fail closed: this split tile's later segments and digest are never written
+                seg = kNoSeg;
                 continue;
             }
-            break;
+            if (b0) load_midstate_sc1(a.seg_state, s_i, lane, st);
+        } else {
+            wt = (uint32_t)t;
+            b0 = ob0;
+            b1 = seg != kNoSeg ? seg_at : 0xFFFFFFFFu;
+            // (overlapped cycles: no chain waits on these tiles, so no queue
+            // order to keep -- the request kernel's progress priorities)
+            pr = a.tile_prio_progress ? kPrioProgress : prio_of(a.steal_own_prio ? q : qq, a.n_queues);
         }
-        if (a.trace && lane == 0) {
-            uint32_t xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            a.trace[3 * t] = __builtin_amdgcn_s_memrealtime();
-            a.trace[3 * t + 2] = (unsigned long long)hw | ((unsigned long long)(xcc & 0xFFu) << 32) |
-                                 ((unsigned long long)qq << 40) | ((unsigned long long)slot << 44);
+        const bool done = hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req,
+                                                       a.req_out, my, wt, lane, pr, b0, b1, st);
+        if (!done && !is_seg) {  // own tile paused at seg_at
+            ob0 = seg_at;
+            continue;
         }
-        hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req, a.req_out, my,
-                                     (uint32_t)t, lane, prio_of(a.steal_own_prio ? q : qq, a.n_queues));
+        if (!done) store_midstate_sc1(a.seg_state, s_i, lane, st);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (a.trace && lane == 0) a.trace[3 * t + 1] = __builtin_amdgcn_s_memrealtime();
-        const uint32_t j0 = a.tadj_first[t], j1 = a.tadj_first[t + 1];
-        for (uint32_t j = j0 + lane; j < j1; j += 64u)
-            __hip_atomic_fetch_add(a.counters + a.tadj[j], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done) {
+            if (!is_seg && a.trace && lane == 0) a.trace[3 * t + 1] = __builtin_amdgcn_s_memrealtime();
+            const uint32_t j0 = a.tadj_first[wt], j1 = a.tadj_first[wt + 1];
+            for (uint32_t j = j0 + lane; j < j1; j += 64u)
+                __hip_atomic_fetch_add(a.counters + a.tadj[j], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (is_seg) {
+            if (lane == 0u)
+                __hip_atomic_store(a.seg_flags + 16u * s_i, a.seg_epoch * a.seg_per_tile + k_i + 1u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            seg = kNoSeg;
+#pragma unroll
+            for (int i = 0; i < 8; i++) st[i] = own_st[64 * i + lane];
+        } else {
+            have = false;
+        }
     }
     fused_retire(a.ctl, lane);
 }

@@ -421,6 +421,12 @@ class Pipeline:
         check(self._lib.mirsha_pipeline_shape(self.handle, ctypes.byref(t), ctypes.byref(c), ctypes.byref(g)))
         return t.value, c.value, g.value
 
+    def split_tiles(self) -> tuple[int, int]:
+        """(split tiles, segments per tile) of a fused plan (mirsha_pipeline_split_tiles)."""
+        n, k = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        check(self._lib.mirsha_pipeline_split_tiles(self.handle, ctypes.byref(n), ctypes.byref(k)))
+        return n.value, k.value
+
     def trace(self) -> np.ndarray | None:
         """Last run's fused timeline (MIRSHA_FUSED_TRACE=1 at plan creation), see include/mirsha.h."""
         n = ctypes.c_uint64(0)

@@ -4,21 +4,26 @@ libmirsha.so (CPU test); on the GPU the program runs with no Python in the
 process and its digests are compared with the golden testengine request
 digests (tests/golden/layouts.json, hashlib-made from the reference's layouts,
 testengine/recorder.go:158-174 and state_machine.go:313-317)."""
+import json
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
+import oracle_py
 from mirbft_amd import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "c", "cgo_sequence.c")
+PATH_SRC = os.path.join(ROOT, "tests", "c", "cgo_path.c")
 
 
-def build(out_dir) -> str:
-    exe = os.path.join(str(out_dir), "cgo_sequence")
-    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    SRC, "-L", _lib.LIB_DIR, "-lmirsha", "-Wl,-rpath," + _lib.LIB_DIR, "-o", exe], check=True)
+def build(out_dir, src=SRC, name="cgo_sequence") -> str:
+    exe = os.path.join(str(out_dir), name)
+    subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-pthread", "-I",
+                    os.path.join(ROOT, "include"), src, "-L", _lib.LIB_DIR, "-lmirsha", "-Wl,-rpath," + _lib.LIB_DIR,
+                    "-o", exe], check=True)
     return exe
 
 
@@ -41,3 +46,27 @@ def test_cgo_sequence_on_gpu(tmp_path, layouts):
     for tag in ("req", "async"):
         got = {int(i): h for t, i, h in (ln.split() for ln in lines if ln.startswith(tag + " "))}
         assert got == want, tag
+
+
+def test_cgo_path_compiles_and_links(tmp_path):
+    exe = build(tmp_path, PATH_SRC, "cgo_path")
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
+    assert "libmirsha.so" in ldd and "not found" not in ldd
+
+
+@pytest.mark.gpu
+def test_cgo_path_on_gpu(tmp_path):
+    """The binding's HashBatch from C (serial and parallel packing of 3 heap
+    slices per request into the pinned arena, then mirsha_hash_batch; and the
+    library-packed mirsha_hash_slices): the legs agree (checked in the
+    program) and the digests are the oracle's."""
+    exe = build(tmp_path, PATH_SRC, "cgo_path")
+    n, data_len = 100_003, 256
+    r = subprocess.run([exe, str(n), str(data_len), "8", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    line = json.loads(r.stdout.splitlines()[-1])
+    assert line["requests"] == n and line["parallel"]["ms"] > 0
+    arena = oracle_py.gen_requests(0x6D69726266740002, 0, 4, data_len)
+    stride = 16 + data_len
+    want = oracle_py.hash_requests(arena, np.arange(4, dtype=np.uint64) * stride, np.full(4, stride))
+    assert line["sample"].split(",") == [w.tobytes().hex() for w in want]

@@ -452,6 +452,8 @@ def test_pipeline_device_full_size(engine, mode, cfg, data_len, n, bs):
         assert plan.mode_name == ("fused" if bs == 500 else "sequential")
     else:
         assert plan.mode_name == mode
+    if plan.mode_name == "fused" and cfg == 3:  # 4,096 tiles > the tile-wave slots: split tiles
+        assert plan.split_tiles()[0] > 0
     d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
     d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
     d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
@@ -558,9 +560,9 @@ def test_pipeline_overlap_irregular_lists(engine):
     plan.close()
 
 
-def _irregular(seed, n=3000, n_lists=300, max_list=60, max_len=600):
+def _irregular(seed, n=3000, n_lists=300, max_list=60, max_len=600, min_len=0):
     rng = np.random.default_rng(seed)
-    lens = rng.integers(0, max_len, n).astype(np.uint32)
+    lens = rng.integers(min_len, max_len, n).astype(np.uint32)
     off = np.zeros(n, dtype=np.uint64)
     np.cumsum(lens[:-1], out=off[1:])
     arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
@@ -660,6 +662,43 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
         if i:
             assert np.array_equal(d_bat.cpu().numpy(), want_bat), f"cycle {i - 1} batches"
     plan.status()
+    plan.close()
+
+
+@pytest.mark.parametrize("pace,n_tiles", [(1, 1100), (2, 2200), (4, 4200)])
+def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles):
+    """More request tiles than the fused launch has tile-wave slots: the
+    overflow tiles run as block-range segments hosted one per SIMD (midstate
+    through memory, sequential flags).  Mixed lengths (split tiles of
+    different block counts than their hosts'), shared / null list entries;
+    three runs on one plan (monotone segment flags), then overlapped cycles
+    and the flush; bit-exact vs the oracle."""
+    torch = _torch()
+    monkeypatch.setenv("MIRSHA_AB", "1")
+    monkeypatch.setenv("MIRSHA_FUSED_PACE", str(pace))
+    arena, off, lens, idx, first = _irregular(60 + pace, 64 * n_tiles - 17, 2048, 60, 1300, 300)
+    plan = engine.pipeline(lens.size, idx, first, lens, mode="fused")
+    n_split, per_tile = plan.split_tiles()
+    assert n_split > 0 and per_tile >= 2, (n_split, per_tile)
+    want_req = oracle_py.hash_requests(arena, off, lens, threads=8)
+    want_lst = oracle_py.batch_digests(want_req, idx, first)
+    for req, lst in _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=3):
+        assert np.array_equal(req, want_req)
+        assert np.array_equal(lst, want_lst)
+    d_arena = torch.from_numpy(arena).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+    d_req = [torch.zeros((lens.size, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_lst = torch.zeros((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    args = (d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr())
+    torch.cuda.synchronize()
+    engine.pipeline_overlap_device(plan, *args, d_req[0].data_ptr(), 0, d_lst.data_ptr())
+    engine.pipeline_overlap_device(plan, *args, d_req[1].data_ptr(), d_req[0].data_ptr(), d_lst.data_ptr())
+    engine.sync()
+    plan.status()
+    assert np.array_equal(d_req[0].cpu().numpy(), want_req)
+    assert np.array_equal(d_req[1].cpu().numpy(), want_req)
+    assert np.array_equal(d_lst.cpu().numpy(), want_lst)
     plan.close()
 
 
