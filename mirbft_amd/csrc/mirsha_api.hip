@@ -156,6 +156,8 @@ struct mirsha_pipeline {
     uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
     uint32_t list_tiles = 0;  // FusedArgs::list_tiles
     uint32_t q_first[mirsha::kFusedMaxQueues + 1] = {};  // tile queues (fused_build)
+    uint32_t q_waves[mirsha::kFusedMaxQueues] = {};      // waves of each queue's slot
+    uint32_t tile_blocks = 0;
     uint64_t epoch = 0;  // completed runs of a fused plan
     DevBuf d_tadj_first, d_tadj, d_cbase, d_expected, d_counters, d_ctl, d_trace;
     // Sticky error word of a fused plan, in host-mapped memory: the launch's
@@ -1090,8 +1092,10 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     uint32_t at = 0;
     for (uint32_t q = 0; q < P; q++) {
         p->q_first[q] = std::min<uint32_t>(p->n_tiles, at);
-        at += 4u * tile_blocks + LB * lb_slot(q);
+        p->q_waves[q] = 4u * tile_blocks + LB * lb_slot(q);
+        at += p->q_waves[q];
     }
+    p->tile_blocks = tile_blocks;
     p->q_first[P] = p->n_tiles;
     // Split tiles (FusedArgs::n_split): tiles beyond the tile waves' slots
     // would run as a fifth tile on some SIMDs (config 3: 72 of 4,096, ending
@@ -1221,6 +1225,8 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.trace = p->trace ? p->d_trace.as<unsigned long long>() : nullptr;
     a.n_counters = p->n_counters;
     for (uint32_t q = 0; q <= mirsha::kFusedMaxQueues; q++) a.q_first[q] = p->q_first[std::min(q, p->pace)];
+    for (uint32_t q = 0; q < mirsha::kFusedMaxQueues; q++) a.q_waves[q] = q < p->pace ? p->q_waves[q] : 0u;
+    a.tile_blocks = p->tile_blocks;
     a.n_queues = p->pace;
     a.steal_own_prio = getenv_flag("MIRSHA_FUSED_STEAL_PRIO") ? 1u : 0u;
     a.list_tiles = p->list_tiles;

@@ -125,6 +125,8 @@ struct FusedArgs {
     unsigned long long* trace;
     uint32_t n_counters;
     uint32_t q_first[kFusedMaxQueues + 1];
+    uint32_t q_waves[kFusedMaxQueues];  // waves serving each queue first (static first tiles); tickets count beyond
+    uint32_t tile_blocks;               // tile blocks in the grid (after the list blocks)
     uint32_t n_queues;  // = tile waves per SIMD (pace)
     uint32_t steal_own_prio;  // A/B (MIRSHA_FUSED_STEAL_PRIO=1): tiles taken from the last queue keep the taker's priority
     // Tile waves in LIST blocks (MIRSHA_FUSED_LIST_TILES): 0 = none (the pair

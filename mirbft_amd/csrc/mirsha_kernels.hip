@@ -1564,6 +1564,18 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             seg_at = (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
         }
     }
+    // The first tile of a wave in its own queue is static: queue q holds one
+    // tile per wave of slot q (a_qw[q]), the wave's index among them below.
+    // Claims on one ticket word saturate near 88 per us (MI355X_MICROARCH.md,
+    // dequeue), so ~1,000 waves per queue claiming at launch waited up to
+    // ~11 us; only the rest (steals, surplus tiles) go through the tickets.
+    uint32_t static_idx = 0xFFFFFFFFu;
+    if (!list_block) {
+        static_idx = (blockIdx.x - a.list_waves) * 4u + simd;
+    } else if (tiles && own) {
+        const uint32_t lbs = a.list_tiles == 1u ? 2u : (q == 0u ? 2u : 4u);  // list-block tile waves of slot q
+        static_idx = a.tile_blocks * 4u + blockIdx.x * lbs + (lbs == 2u ? simd - 2u : simd);
+    }
     uint64_t t = 0;
     bool have = false;    // a claimed own tile in progress
     uint32_t ob0 = 0u;    // its next block
@@ -1575,7 +1587,14 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     while (true) {
         if (!have && tiles) {
             qq = own ? q : last;
-            const uint64_t c = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) + a.q_first[qq];
+            uint64_t c;
+            if (own && static_idx < a.q_waves[qq]) {
+                c = a.q_first[qq] + static_idx;
+                static_idx = 0xFFFFFFFFu;
+            } else {
+                static_idx = 0xFFFFFFFFu;
+                c = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) + a.q_first[qq] + a.q_waves[qq];
+            }
             if (c >= a.q_first[qq + 1]) {
                 if (own && qq != last) {
                     own = false;

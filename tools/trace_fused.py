@@ -49,8 +49,10 @@ def main():
         chunk = tr[3 * nt:3 * nt + nc]
         gend = tr[3 * nt + nc:3 * nt + nc + ng]
         cend = tr[3 * nt + nc + ng:3 * nt + 2 * nc + ng]
-        queue, slot = (info >> 40) & 0xF, (info >> 44) & 0xF
+        traced = ts > 0  # split tiles run as segments and carry no tile stamps
+        ts, te, info = ts[traced], te[traced], info[traced]
         simd_key = ((info >> 32) & 0xFF) << 16 | ((info & 0xFFFFFFFF) >> 4) & 0xFFF
+        queue, slot = (info >> 40) & 0xF, (info >> 44) & 0xF
         t0 = ts.min()
         us = lambda x: (x - t0) / 100.0  # noqa: E731  (100 MHz ticks -> us)
         dur = (te - ts) / 100.0
