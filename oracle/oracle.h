@@ -93,6 +93,8 @@ void oracle_gen_requests(uint64_t seed, uint64_t first, uint64_t count, uint32_t
  * Message = LE64(i % 16) || LE64(i / 16) || data (bytes as oracle_gen_requests). */
 #define ORACLE_LEN_TAG 0x4C454E4754480000ull
 uint32_t oracle_mixed_data_len(uint64_t seed, uint64_t i);
+/* Request lengths (16-byte header + data) of requests [first, first + n). */
+void oracle_mixed_lengths(uint64_t seed, uint64_t first, uint64_t n, uint32_t* len_out);
 /* Messages for the request ids[k] (any order), packed densely in that order:
  * off_out[k] / len_out[k] = offset / message length (16 + data_len) of ids[k]. */
 void oracle_gen_mixed(uint64_t seed, const uint64_t* ids, uint64_t n, uint8_t* arena, uint64_t* off_out,

@@ -312,6 +312,10 @@ uint32_t oracle_mixed_data_len(uint64_t seed, uint64_t i) {
     return (uint32_t)((64ull << e) + (((64ull << e) * m) >> 24));
 }
 
+void oracle_mixed_lengths(uint64_t seed, uint64_t first, uint64_t n, uint32_t* len_out) {
+    for (uint64_t r = 0; r < n; r++) len_out[r] = 16u + oracle_mixed_data_len(seed, first + r);
+}
+
 void oracle_gen_mixed(uint64_t seed, const uint64_t* ids, uint64_t n, uint8_t* arena, uint64_t* off_out,
                       uint32_t* len_out) {
     uint64_t p = 0;

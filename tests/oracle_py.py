@@ -41,6 +41,7 @@ def load() -> ctypes.CDLL:
     lib.oracle_mixed_data_len.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
     lib.oracle_mixed_data_len.restype = ctypes.c_uint32
     lib.oracle_gen_mixed.argtypes = [ctypes.c_uint64, vp, ctypes.c_uint64, vp, vp, vp]
+    lib.oracle_mixed_lengths.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, vp]
     lib.oracle_splitmix64.argtypes = [ctypes.c_uint64]
     lib.oracle_splitmix64.restype = ctypes.c_uint64
     _lib = lib
@@ -106,6 +107,14 @@ def gen_requests(seed: int, first: int, count: int, data_len: int) -> np.ndarray
 def mixed_data_len(seed: int, i: int) -> int:
     """BASELINE config 5 data length of request i (oracle.h, oracle_mixed_data_len)."""
     return int(load().oracle_mixed_data_len(seed, i))
+
+
+def mixed_lengths(seed: int, first: int, count: int) -> np.ndarray:
+    """Request lengths (header + data) of config-5 requests [first, first + count)."""
+    out = np.empty(count, dtype=np.uint32)
+    if count:
+        load().oracle_mixed_lengths(seed, first, count, _p(out))
+    return out
 
 
 def gen_mixed(seed: int, ids) -> tuple[np.ndarray, np.ndarray, np.ndarray]:

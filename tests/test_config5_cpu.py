@@ -6,6 +6,7 @@ import hashlib
 import numpy as np
 
 import oracle_py
+from mirbft_amd import sharding
 
 SEED5 = 0x6D69726266740005
 MASK = (1 << 64) - 1
@@ -54,3 +55,25 @@ def test_generated_messages_hash_like_hashlib():
         assert ln[k] == len(msg)
         assert bytes(arena[off[k]:off[k] + ln[k]]) == msg
         assert got[k].tobytes() == hashlib.sha256(msg).digest()
+
+
+def test_world8_block_balanced_cuts_of_the_1e8_stream():
+    """BASELINE config 5's 10^8-request stream cut for 8 GPUs by the
+    block-balanced sharder (bench.py, tests/test_gpu_config5.py): contiguous,
+    covering ranges whose compression counts are each within one request's
+    compressions (a 64 KB request: 1,025) of the fair share."""
+    n, world = 10**8, 8
+    lens = oracle_py.mixed_lengths(SEED5, 0, n)
+    assert lens.min() >= 16 + 64 and lens.max() < 16 + 65536
+    cuts = sharding.shard_ranges(n, world, 1, lens)
+    assert cuts[0][0] == 0 and cuts[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(cuts, cuts[1:]))
+    blk = sharding.blocks_for_len(lens).astype(np.int64)
+    del lens
+    cum = np.concatenate([[0], np.cumsum(blk)])
+    fair = cum[-1] / world
+    one = int(blk.max())
+    shares = [int(cum[hi] - cum[lo]) for lo, hi in cuts]
+    assert max(abs(s - fair) for s in shares) <= one, (shares, fair, one)
+    # every shard near 12.5 M requests (the per-GPU workload of bench.py --config 5)
+    assert all(abs((hi - lo) - n // world) < 0.01 * n // world for lo, hi in cuts), cuts
