@@ -187,6 +187,9 @@ int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
  * H2D, kernels and D2H overlap): there pack = host time spent packing, device
  * = host time spent waiting on the device, scatter = copying digests out, and
  * the phases overlap the DMA rather than add up.  total = the whole call.
+ * Asynchronous submissions (mirsha_submit_slices): every phase belongs to the
+ * most recently COMPLETED ticket (published when it retires: mirsha_wait,
+ * mirsha_poll, or a later submission reusing its ring slot); total = 0.
  * Writes min(n, phases) entries; returns the number of phases. */
 #define MIRSHA_PROF_VALIDATE 0
 #define MIRSHA_PROF_PLAN 1
@@ -353,6 +356,9 @@ int mirsha_chains_reset(mirsha_ctx* ctx, mirsha_chains* chains, const uint32_t* 
 int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena,
                             uint64_t arena_len, const uint64_t* off, const uint32_t* len,
                             uint32_t n, uint8_t* digests_out);
+/* Contexts mirsha_hash_batch_multi keeps per device between calls: freed here
+ * (optional; otherwise at process exit). */
+void mirsha_multi_release(void);
 
 /* ------------------------------------------- benchmark / test utility only */
 /* Device-side synthetic request stream, byte-identical to the

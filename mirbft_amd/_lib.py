@@ -100,6 +100,7 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p],
     ),
+    "mirsha_multi_release": (None, []),
     "mirsha_synth_requests_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint32, c_void_p]),
     "mirsha_synth_mixed_lengths_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p]),
     "mirsha_synth_mixed_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p]),

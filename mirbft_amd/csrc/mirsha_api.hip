@@ -97,6 +97,7 @@ struct AsyncSlot {
     uint8_t* user_out = nullptr;
     uint32_t n = 0, m = 0;
     std::vector<uint32_t> rank;  // request -> row of `dig` (empty: identity)
+    double prof[MIRSHA_PROF_PHASES] = {};  // this submission's host phases (published when it completes)
 };
 
 struct KernelTimer {
@@ -657,11 +658,18 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         HIP_TRY(c, hipEventRecord(ev_out[k], c->xout));
         // digests that are already back go to the caller while later chunks pack
         uint32_t ready = copied;
-        while (ready < k && hipEventQuery(ev_out[ready]) == hipSuccess) ready++;
+        while (ready < k) {
+            const hipError_t q = hipEventQuery(ev_out[ready]);
+            if (q == hipErrorNotReady) {
+                (void)hipGetLastError();  // NotReady is not an error; never let a later launch check see it
+                break;
+            }
+            if (q != hipSuccess) return fail(c, MIRSHA_EHIP, "hipEventQuery: %s", hipGetErrorString(q));
+            ready++;
+        }
         copy_out(copied, ready);
         copied = ready;
     }
-    (void)hipGetLastError();  // hipEventQuery's hipErrorNotReady
     if (n_lists) {
         HIP_TRY(c, c->d_scratch.ensure(sizeof(uint32_t) * std::max<uint32_t>(entries, 1)));
         if (int rc = timed_launch(c, 1, [&] {
@@ -1365,7 +1373,7 @@ int slice_lengths(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t
 int async_complete(mirsha_ctx* c, AsyncSlot& sl) {
     HIP_TRY(c, hipEventSynchronize(sl.done));
     const auto t_done = Clock::now();
-    c->prof[MIRSHA_PROF_DEVICE] = std::chrono::duration<double, std::milli>(t_done - sl.t_queued).count();
+    sl.prof[MIRSHA_PROF_DEVICE] = std::chrono::duration<double, std::milli>(t_done - sl.t_queued).count();
     const uint8_t* d = sl.dig.as<uint8_t>();
     if (sl.rank.empty()) {
         memcpy(sl.user_out, d, 32ull * sl.n);
@@ -1374,7 +1382,11 @@ int async_complete(mirsha_ctx* c, AsyncSlot& sl) {
     }
     sl.busy = false;
     c->done_ticket = std::max(c->done_ticket, sl.ticket);
-    c->prof[MIRSHA_PROF_SCATTER] = ms_since(t_done);
+    sl.prof[MIRSHA_PROF_SCATTER] = ms_since(t_done);
+    sl.prof[MIRSHA_PROF_CHUNKS] = 0;
+    // mirsha_ctx_host_profile: every phase of ONE submission, the most
+    // recently completed (not one ticket's plan beside another's device time)
+    for (int k = 0; k < MIRSHA_PROF_PHASES; k++) c->prof[k] = sl.prof[k];
     return MIRSHA_OK;
 }
 
@@ -1394,7 +1406,6 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
                  uint32_t* n_unique_out) {
     if (flags & ~MIRSHA_SUBMIT_DEDUP) return fail(c, MIRSHA_EINVAL, "unknown submit flags 0x%x", flags);
     auto t0 = Clock::now();
-    for (double& x : c->prof) x = 0.0;
     // Which requests reach the GPU: all, or one per distinct content.  With
     // dedup the fingerprint heads (every one of them a final representative)
     // are packed and queued first; the byte-for-byte confirmation of the
@@ -1403,6 +1414,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     // in a second launch.  The fingerprints are taken in the validation walk
     // over the slice arrays (dedup_candidates_checked): one pass, not two.
     const bool dedup = (flags & MIRSHA_SUBMIT_DEDUP) && n > 1;
+    double ph[MIRSHA_PROF_PHASES] = {};
     std::vector<uint32_t> len;
     std::vector<uint32_t> which;  // requests in digest-row order (empty = all, identity)
     std::vector<uint64_t> fp;
@@ -1423,7 +1435,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     } else if (n) {
         if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     }
-    c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
+    ph[MIRSHA_PROF_VALIDATE] = ms_since(t0);
     t0 = Clock::now();
     if (int rc = use_device(c)) return rc;
     AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
@@ -1435,7 +1447,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
         for (uint32_t i = 0; i < n; i++)
             if (tent[i] == i) which.push_back(i);
     }
-    c->prof[MIRSHA_PROF_PLAN] = ms_since(t0);
+    ph[MIRSHA_PROF_PLAN] = ms_since(t0);
     t0 = Clock::now();
     HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
     if (!sl.done) HIP_TRY(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
@@ -1482,7 +1494,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     };
     uint32_t m = dedup ? (uint32_t)which.size() : n;
     if (int rc = queue(dedup ? which.data() : nullptr, m, 0)) return rc;
-    c->prof[MIRSHA_PROF_PACK] = ms_since(t0);
+    ph[MIRSHA_PROF_PACK] = ms_since(t0);
     sl.t_queued = Clock::now();
     if (dedup) {
         t0 = Clock::now();
@@ -1505,7 +1517,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
         }
         for (uint32_t i = 0; i < n; i++) sl.rank[i] = sl.rank[rep[i]];
         if (heads_only && m == n) sl.rank.clear();  // all distinct: rows are already in origin order
-        c->prof[MIRSHA_PROF_PLAN] += ms_since(t0);
+        ph[MIRSHA_PROF_PLAN] += ms_since(t0);
     }
     if (n_unique_out) *n_unique_out = m;
     HIP_TRY(c, hipEventRecord(sl.done, c->stream));
@@ -1514,6 +1526,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     sl.n = n;
     sl.m = m;
     sl.ticket = c->next_ticket++;
+    for (int k = 0; k < MIRSHA_PROF_PHASES; k++) sl.prof[k] = ph[k];
     if (ticket_out) *ticket_out = sl.ticket;
     return MIRSHA_OK;
 }
@@ -1741,7 +1754,10 @@ int mirsha_poll(mirsha_ctx* c, uint64_t ticket, int* done) {
     for (uint64_t t = c->done_ticket + 1; t <= ticket; t++) {
         AsyncSlot& sl = c->slots[(t - 1) % kAsyncSlots];
         const hipError_t q = hipEventQuery(sl.done);
-        if (q == hipErrorNotReady) return MIRSHA_OK;
+        if (q == hipErrorNotReady) {
+            (void)hipGetLastError();  // not an error (see run_pipelined)
+            return MIRSHA_OK;
+        }
         if (q != hipSuccess) return fail(c, MIRSHA_EHIP, "hipEventQuery: %s", hipGetErrorString(q));
     }
     if (int rc = async_wait_upto(c, ticket)) return rc;
@@ -2183,6 +2199,43 @@ int mirsha_clock_probe(mirsha_ctx* c, uint32_t iters, double* clock_ghz, double*
     return MIRSHA_OK;
 }
 
+// Per-device contexts of mirsha_hash_batch_multi, kept across calls (a
+// context owns streams, events and grown staging buffers: creating one per
+// call per device cost a stream setup and a cold staging path every time).
+// A device listed twice in one call takes two contexts.  Released by
+// mirsha_multi_release (or at process exit).
+namespace {
+std::mutex g_multi_mu;
+std::vector<mirsha_ctx*> g_multi_idle;
+}  // namespace
+
+static int multi_ctx_take(int device, mirsha_ctx** out) {
+    {
+        std::lock_guard<std::mutex> lk(g_multi_mu);
+        for (size_t i = 0; i < g_multi_idle.size(); i++)
+            if (g_multi_idle[i]->device == device) {
+                *out = g_multi_idle[i];
+                g_multi_idle.erase(g_multi_idle.begin() + (ptrdiff_t)i);
+                return MIRSHA_OK;
+            }
+    }
+    return mirsha_ctx_create(device, out);
+}
+
+static void multi_ctx_give(mirsha_ctx* c) {
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    g_multi_idle.push_back(c);
+}
+
+void mirsha_multi_release(void) {
+    std::vector<mirsha_ctx*> v;
+    {
+        std::lock_guard<std::mutex> lk(g_multi_mu);
+        v.swap(g_multi_idle);
+    }
+    for (mirsha_ctx* c : v) mirsha_ctx_destroy(c);
+}
+
 int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena, uint64_t arena_len,
                             const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* out) {
     if (ndev <= 0 || !devices) return MIRSHA_EINVAL;
@@ -2206,10 +2259,10 @@ int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena, 
             const uint32_t a = cut[k], b = cut[k + 1];
             if (a >= b) return;
             mirsha_ctx* c = nullptr;
-            int rc = mirsha_ctx_create(devices[k], &c);
+            int rc = multi_ctx_take(devices[k], &c);
             if (rc == MIRSHA_OK) rc = mirsha_hash_batch(c, arena, arena_len, off + a, len + a, b - a, out + 32ull * a);
             rcs[k] = rc;
-            mirsha_ctx_destroy(c);
+            if (c) multi_ctx_give(c);
         });
     }
     for (auto& t : th) t.join();
