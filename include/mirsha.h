@@ -268,6 +268,10 @@ int mirsha_digest_lists_device(mirsha_ctx* ctx, const uint8_t* d_digests, uint32
 #define MIRSHA_PIPELINE_SEQUENTIAL 0
 #define MIRSHA_PIPELINE_FUSED 1
 #define MIRSHA_PIPELINE_AUTO 3
+/* Deprecated (round 1; kept one release so old callers still compile): the
+ * retired modes.  mirsha_pipeline_create_mode returns MIRSHA_EINVAL for them. */
+#define MIRSHA_PIPELINE_STREAMS 2
+#define MIRSHA_PIPELINE_CONT 4
 typedef struct mirsha_pipeline mirsha_pipeline;
 int mirsha_pipeline_create(mirsha_ctx* ctx, uint32_t n_req, const uint32_t* len, const uint32_t* idx,
                            const uint32_t* list_first, uint32_t n_lists, mirsha_pipeline** out);
@@ -297,6 +301,10 @@ int mirsha_pipeline_status(mirsha_ctx* ctx, mirsha_pipeline* p);
  * [3 n_tiles + n_counters + g].  *words = total length (0 when tracing is off). */
 int mirsha_pipeline_trace(mirsha_ctx* ctx, mirsha_pipeline* p, uint64_t* out, uint64_t cap, uint64_t* words);
 int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t* n_counters, uint32_t* n_groups);
+/* Deprecated (round 1's chain-segment mode, retired): kept one release so old
+ * callers still link.  Every plan is one segment: *n_segments = 1 and, if
+ * cap >= 1, bounds[0] = 0. */
+int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap);
 /* Split tiles of a fused plan: request tiles beyond the launch's tile-wave
  * slots, each run as *segments_per_tile sequential block-range segments
  * spread one per SIMD (0, 0 when none). */

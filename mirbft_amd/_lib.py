@@ -83,6 +83,7 @@ SIGNATURES = {
     "mirsha_pipeline_trace": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "mirsha_pipeline_shape": (c_int, [c_void_p, _u32p, _u32p, _u32p]),
     "mirsha_pipeline_split_tiles": (c_int, [c_void_p, _u32p, _u32p]),
+    "mirsha_pipeline_segments": (c_int, [c_void_p, _u32p, _u32p, c_uint32]),
     "mirsha_hash_requests_then_batches_device": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p],

@@ -157,6 +157,7 @@ struct mirsha_pipeline {
     uint32_t pace = 1, list_blocks = 0, tile_waves = 0;  // tile waves per SIMD; list blocks first in the grid
     uint32_t list_tiles = 0;  // FusedArgs::list_tiles
     uint32_t q_first[mirsha::kFusedMaxQueues + 1] = {};  // tile queues (fused_build)
+    uint32_t q_end[mirsha::kFusedMaxQueues] = {};        // queue q = [q_first[q], q_end[q])
     uint32_t q_waves[mirsha::kFusedMaxQueues] = {};      // waves of each queue's slot
     uint32_t tile_blocks = 0;
     uint64_t epoch = 0;  // completed runs of a fused plan
@@ -168,7 +169,7 @@ struct mirsha_pipeline {
     unsigned long long* d_err = nullptr;
     unsigned long long watchdog = mirsha::kFusedWatchdogTicks;
     // split tiles (FusedArgs::n_split)
-    uint32_t n_split = 0, seg_per_tile = 0, seg_nominal_nb = 0;
+    uint32_t n_split = 0, split_first = 0, seg_per_tile = 0, seg_nominal_nb = 0;
     std::vector<uint32_t> seg_nb;
     DevBuf d_seg_nb, d_seg_state, d_seg_flags;
     uint64_t seg_runs = 0;  // launches of the plan (segment flags are monotone over them)
@@ -1105,6 +1106,7 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     }
     p->tile_blocks = tile_blocks;
     p->q_first[P] = p->n_tiles;
+    for (uint32_t q = 0; q < P; q++) p->q_end[q] = p->q_first[q + 1];
     // Split tiles (FusedArgs::n_split): tiles beyond the tile waves' slots
     // would run as a fifth tile on some SIMDs (config 3: 72 of 4,096, ending
     // ~130 us after the rest, profiles/r02af).  Instead each is cut into
@@ -1125,19 +1127,32 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
         // nom = the median block count of the hosts' own tiles (the last
         // queue's).  Only a schedule: a host whose own tile is shorter runs
         // its segment after that tile.
+        // Which tiles split: with 2+ queues the first ns of the last queue.
+        // Their chains of segments end before the last queue's tiles (the
+        // hosts ARE that queue's waves), so in needed-at order they go before
+        // it: the lists' final stretch, computed after the last tiles land,
+        // is then only the last queue's positions.  With one queue, the last.
+        const uint32_t sf = P >= 2 ? p->q_first[P - 1] : p->n_tiles - ns;
         std::vector<uint32_t> own;
-        for (uint32_t t = p->q_first[P - 1]; t < p->n_tiles - ns; t++) own.push_back(tile_blocks_of(t));
+        for (uint32_t t = p->q_first[P - 1]; t < p->n_tiles; t++)
+            if (t < sf || t >= sf + ns) own.push_back(tile_blocks_of(t));
         std::vector<uint32_t> snb;
-        for (uint32_t t = p->n_tiles - ns; t < p->n_tiles; t++) snb.push_back(tile_blocks_of(t));
+        for (uint32_t t = sf; t < sf + ns; t++) snb.push_back(tile_blocks_of(t));
         const uint32_t smax = *std::max_element(snb.begin(), snb.end());
         const uint32_t S = std::min(hosts / ns, smax);
         if (S >= 2 && !own.empty()) {
             std::nth_element(own.begin(), own.begin() + own.size() / 2, own.end());
             p->n_split = ns;
+            p->split_first = sf;
             p->seg_per_tile = S;
             p->seg_nominal_nb = std::max(1u, own[own.size() / 2]);
             p->seg_nb = snb;
-            p->q_first[P] = p->n_tiles - ns;
+            if (P >= 2) {
+                p->q_first[P - 1] += ns;  // (q_end[P - 2] stays sf: the split tiles belong to no queue)
+            } else {
+                p->q_first[P] = p->n_tiles - ns;
+                p->q_end[0] = p->n_tiles - ns;
+            }
         }
     }
     // Device copies.
@@ -1233,6 +1248,7 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.trace = p->trace ? p->d_trace.as<unsigned long long>() : nullptr;
     a.n_counters = p->n_counters;
     for (uint32_t q = 0; q <= mirsha::kFusedMaxQueues; q++) a.q_first[q] = p->q_first[std::min(q, p->pace)];
+    for (uint32_t q = 0; q < mirsha::kFusedMaxQueues; q++) a.q_end[q] = q < p->pace ? p->q_end[q] : p->n_tiles;
     for (uint32_t q = 0; q < mirsha::kFusedMaxQueues; q++) a.q_waves[q] = q < p->pace ? p->q_waves[q] : 0u;
     a.tile_blocks = p->tile_blocks;
     a.n_queues = p->pace;
@@ -1248,6 +1264,7 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.n_groups = (overlap && !overlap_prev) ? 0u : p->n_groups;
     a.list_waves = p->list_blocks;
     a.n_split = p->n_split;
+    a.split_first = p->split_first;
     a.seg_per_tile = p->seg_per_tile;
     a.seg_nominal_nb = p->seg_nominal_nb;
     a.seg_epoch = p->seg_runs;
@@ -1881,6 +1898,13 @@ int mirsha_pipeline_shape(const mirsha_pipeline* p, uint32_t* n_tiles, uint32_t*
     *n_tiles = p->n_tiles;
     *n_counters = p->n_counters;
     *n_groups = p->n_groups;
+    return MIRSHA_OK;
+}
+
+int mirsha_pipeline_segments(const mirsha_pipeline* p, uint32_t* n_segments, uint32_t* bounds, uint32_t cap) {
+    if (!p || !n_segments) return MIRSHA_EINVAL;
+    *n_segments = 1;
+    if (bounds && cap >= 1) bounds[0] = 0;
     return MIRSHA_OK;
 }
 

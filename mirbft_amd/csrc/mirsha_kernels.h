@@ -125,6 +125,7 @@ struct FusedArgs {
     unsigned long long* trace;
     uint32_t n_counters;
     uint32_t q_first[kFusedMaxQueues + 1];
+    uint32_t q_end[kFusedMaxQueues];  // queue q = [q_first[q], q_end[q]); split tiles lie in no queue
     uint32_t q_waves[kFusedMaxQueues];  // waves serving each queue first (static first tiles); tickets count beyond
     uint32_t tile_blocks;               // tile blocks in the grid (after the list blocks)
     uint32_t n_queues;  // = tile waves per SIMD (pace)
@@ -142,8 +143,9 @@ struct FusedArgs {
     // chunk is ready at epoch x expected; 64-bit so it never wraps.
     unsigned long long epoch;
     uint32_t n_tiles, n_groups, list_waves;
-    // Split tiles: the last n_split tiles in needed-at order (those the tile
-    // waves' slots cannot take, e.g. config 3's 4,096 tiles on 4,024 slots)
+    // Split tiles: n_split tiles the tile waves' slots cannot take (config 3's
+    // 4,096 tiles on 4,024 slots), placed just before the last queue in
+    // needed-at order (after it with one queue)
     // run as seg_per_tile sequential block-range segments, segment k of split
     // tile s hosted by the last queue's wave h = s * seg_per_tile + k of the
     // tile blocks (h = (block - list blocks) * 4 + SIMD), which runs it when
@@ -152,7 +154,7 @@ struct FusedArgs {
     // completion through seg_flags[16 s] (monotone: run seg_epoch, segment k
     // done at seg_epoch * seg_per_tile + k + 1).  So no SIMD takes a fifth
     // tile: the overflow spreads as one short segment per SIMD.
-    uint32_t n_split, seg_per_tile, seg_nominal_nb;
+    uint32_t n_split, split_first, seg_per_tile, seg_nominal_nb;  // split tiles [split_first, + n_split)
     // Overlapped cycles: tile waves at the request kernel's progress
     // priorities instead of their queue's (nothing waits on this run's tiles).
     uint32_t tile_prio_progress;

@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
                 static_idx = 0xFFFFFFFFu;
                 c = claim(a.ctl + kCtlTileTicket + 16u * qq, lane) + a.q_first[qq] + a.q_waves[qq];
             }
-            if (c >= a.q_first[qq + 1]) {
+            if (c >= a.q_end[qq]) {
                 if (own && qq != last) {
                     own = false;
                     continue;
@@ -1630,7 +1630,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             s_i = seg / a.seg_per_tile;
             k_i = seg % a.seg_per_tile;
             const uint32_t S = a.seg_per_tile, nbs = a.seg_nb[s_i];
-            wt = a.n_tiles - a.n_split + s_i;
+            wt = a.split_first + s_i;
             b0 = k_i * nbs / S;
             b1 = k_i + 1u == S ? 0xFFFFFFFFu : (k_i + 1u) * nbs / S;
             pr = 3u;  // a segment chain is sequential: run it at the top issue priority
