@@ -50,7 +50,8 @@ def main():
     except (OSError, ValueError):
         tf = {}
     entries = [e for e in tf.get("entries", [])
-               if not (e.get("key") == entry["key"] and e.get("config") == entry["config"])]
+               if not (e.get("key") == entry["key"] and e.get("config") == entry["config"]
+                       and e.get("kernel") == entry["kernel"])]
     entries.append(entry)
     out = {"method": "rocprofv3 --pmc passes over bench.py (profiles/profile.sh); bytes per launch = "
                      "32*TCC_EA0_RDREQ_32B + 64*TCC_EA0_RDREQ_64B + 128*TCC_EA0_RDREQ_128B + WRITE_SIZE*1024 "
