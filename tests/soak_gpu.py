@@ -5,7 +5,8 @@ host arenas with gaps and odd alignments, sliced requests with duplicates
 (plain and dedup), async submit / wait in shuffled order, request -> list
 digests (nulls, empty and shared lists) through the host call and through
 device plans in every mode, tile-queue count and list-tile form, overlapped
-cycles, launches of 65K-400K requests, checkpoint chains -- each checked bit for bit against the oracle (test infrastructure,
+cycles, launches of 65K-400K requests, fused plans with split tiles,
+checkpoint chains -- each checked bit for bit against the oracle (test infrastructure,
 oracle/).  Prints a progress line every ~15 s; exits 1 at the first mismatch
 with the seed that reproduces it.
 
@@ -194,6 +195,57 @@ def case_large(eng, rng, seed):
     plan.close()
 
 
+def case_split(eng, rng, seed):
+    """Fused plans with more tiles than tile-wave slots (split tiles run as
+    block-range segments, FusedArgs::n_split): 1-4 tile queues, a few to a
+    few hundred tiles over capacity, mixed lengths, shared / null list
+    entries; ordinary runs, then overlapped cycles and the flush."""
+    pace = int(rng.integers(1, 5))
+    n_tiles = pace * 1006 + int(rng.integers(1, 400))
+    n = 64 * n_tiles - int(rng.integers(0, 64))
+    ln = rng.integers(int(rng.integers(0, 300)), 1300, n).astype(np.uint32)
+    arena, off = arena_for(rng, ln)
+    idx, first = lists_for(rng, n, int(rng.integers(200, 3000)))
+    os.environ["MIRSHA_AB"] = "1"
+    os.environ["MIRSHA_FUSED_PACE"] = str(pace)
+    plan = eng.pipeline(n, idx, first, ln, mode="fused")
+    os.environ.pop("MIRSHA_FUSED_PACE")
+    os.environ.pop("MIRSHA_AB")
+    want = oracle_py.hash_requests(arena, off, ln, threads=8)
+    want_l = oracle_py.batch_digests(want, idx, first)
+    d_arena = torch.from_numpy(arena).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(ln.view(np.int32)).cuda()
+    nl = first.size - 1
+    d_req = [torch.zeros((n, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_lst = torch.zeros((max(nl, 1), 32), dtype=torch.uint8, device="cuda")
+    args = (d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr())
+    tag = f"split pace={pace} tiles={n_tiles} split={plan.split_tiles()}"
+    for _ in range(2):
+        d_req[0].zero_()
+        d_lst.zero_()
+        torch.cuda.synchronize()
+        eng.hash_requests_then_batches_device(plan, *args, d_req[0].data_ptr(), d_lst.data_ptr())
+        plan.status()
+        check(np.array_equal(d_req[0].cpu().numpy(), want), tag + ": requests", seed)
+        check(np.array_equal(d_lst.cpu().numpy()[:nl], want_l), tag + ": lists", seed)
+    for i in range(3):
+        prev = d_req[(i + 1) % 2].data_ptr() if i else 0
+        d_lst.zero_()
+        torch.cuda.synchronize()
+        if i < 2:
+            eng.pipeline_overlap_device(plan, *args, d_req[i % 2].data_ptr(), prev, d_lst.data_ptr())
+        else:
+            eng.pipeline_overlap_device(plan, 0, 0, 0, 0, 0, prev, d_lst.data_ptr())
+        eng.sync()
+        if i < 2:
+            check(np.array_equal(d_req[i % 2].cpu().numpy(), want), tag + ": overlap requests", seed)
+        if i:
+            check(np.array_equal(d_lst.cpu().numpy()[:nl], want_l), tag + ": overlap lists", seed)
+    plan.status()
+    plan.close()
+
+
 def case_chains(eng, rng, seed):
     """Streaming checkpoint chains (mirsha_chains_*) against hashlib streaming
     hashers: uniform and skewed writes (one chain taking most digests), sums of
@@ -233,15 +285,15 @@ def main():
     a = ap.parse_args()
     eng = Engine(0)
     t0 = last = time.time()
-    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0, "chains": 0}
+    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0, "chains": 0, "split": 0}
     k = 0
     while time.time() - t0 < a.seconds:
         seed = a.seed * 1_000_003 + k
         rng = np.random.default_rng(seed)
-        which = ("host", "slices", "plan", "host", "slices", "plan", "large", "chains")[k % 8]
+        which = ("host", "slices", "plan", "host", "slices", "plan", "large", "chains", "split")[k % 9]
         try:
             {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large,
-             "chains": case_chains}[which](eng, rng, seed)
+             "chains": case_chains, "split": case_split}[which](eng, rng, seed)
         except AssertionError as e:
             print(e, flush=True)
             sys.exit(1)

@@ -1,0 +1,7 @@
+#!/bin/bash
+# r03o: randomised soak (split-tile case added) for 240 s.
+set -uo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r03o; mkdir -p $O
+timeout -k 10 330 python -u tests/soak_gpu.py --seconds 240 --seed 31 > $O/soak.log 2>&1 || { tail -20 $O/soak.log; exit 1; }
+tail -3 $O/soak.log
