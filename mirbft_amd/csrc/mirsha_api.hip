@@ -91,6 +91,8 @@ struct AsyncSlot {
     Clock::time_point t_queued;  // when its device work was queued
     PinnedBuf dig;    // m x 32 digests (D2H target)
     DevBuf dev;       // the same layout as stage, then m x 32 digests
+    PinnedBuf stage2;  // a dedup submission's second launch (representatives
+    DevBuf dev2;       // found after the first), queued behind the first
     hipEvent_t done = nullptr;
     uint64_t ticket = 0;
     bool busy = false;
@@ -1424,31 +1426,20 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     if (flags & ~MIRSHA_SUBMIT_DEDUP) return fail(c, MIRSHA_EINVAL, "unknown submit flags 0x%x", flags);
     auto t0 = Clock::now();
     // Which requests reach the GPU: all, or one per distinct content.  With
-    // dedup the fingerprint heads (every one of them a final representative)
-    // are packed and queued first; the byte-for-byte confirmation of the
-    // duplicates then runs on the host while the GPU hashes the heads, and
-    // representatives found only there (fingerprint collisions, rare) follow
-    // in a second launch.  The fingerprints are taken in the validation walk
-    // over the slice arrays (dedup_candidates_checked): one pass, not two.
+    // dedup the requests are scanned in segments in origin order
+    // (mirsha::host::DedupScan): the first segment's heads (distinct
+    // contents, each a final representative) are packed and queued as soon as
+    // that segment is scanned, and the GPU hashes them while the host scans
+    // and confirms the rest -- a request matching an earlier head is compared
+    // byte for byte in the same walk, while its bytes are cache-warm.
+    // Representatives found later (new contents of later segments, and
+    // fingerprint collisions, rare) follow in one second launch.
     const bool dedup = (flags & MIRSHA_SUBMIT_DEDUP) && n > 1;
     double ph[MIRSHA_PROF_PHASES] = {};
     std::vector<uint32_t> len;
-    std::vector<uint32_t> which;  // requests in digest-row order (empty = all, identity)
-    std::vector<uint64_t> fp;
-    std::vector<uint32_t> tent;
-    std::vector<uint64_t> rl;
-    uint32_t heads = 0;
     if (dedup) {
         if (int rc = slice_args(c, slice_ptr, slice_len, slice_first, n, out)) return rc;
-        rl.resize(n);
-        fp.resize(n);
-        tent.resize(n);
-        std::vector<uint8_t> err(n);
-        if (!mirsha::host::dedup_candidates_checked(slice_ptr, slice_len, slice_first, n, slice_first[n],
-                                                    MIRSHA_MAX_MESSAGE_BYTES, rl.data(), err.data(), fp.data(),
-                                                    tent.data(), &heads))
-            return slice_errors(c, err.data(), n);
-        len.assign(rl.begin(), rl.end());
+        len.assign(n, 0u);
     } else if (n) {
         if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     }
@@ -1459,18 +1450,13 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     if (sl.busy)
         if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
     sl.rank.clear();
-    if (dedup) {
-        which.reserve(heads);
-        for (uint32_t i = 0; i < n; i++)
-            if (tent[i] == i) which.push_back(i);
-    }
-    ph[MIRSHA_PROF_PLAN] = ms_since(t0);
-    t0 = Clock::now();
     HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
     if (!sl.done) HIP_TRY(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-    // Packs requests `ids` (identity when null) and queues their digests into
-    // rows [row0, row0 + m) of sl.dig.
-    auto queue = [&](const uint32_t* ids, uint32_t m, uint32_t row0) -> int {
+    ph[MIRSHA_PROF_PLAN] = ms_since(t0);
+    // Packs requests `ids` (identity when null) into `stage`, and queues their
+    // digests into rows [row0, row0 + m) of sl.dig.
+    auto queue = [&](const uint32_t* ids, uint32_t m, uint32_t row0, PinnedBuf& stage, DevBuf& dev) -> int {
+        const auto tq = Clock::now();
         std::vector<uint64_t> poff(m);
         std::vector<uint32_t> plen(m);
         uint64_t bytes = 0;
@@ -1486,15 +1472,15 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
         const uint64_t o_off = align8(bytes + kArenaSlack);
         const uint64_t o_len = o_off + 8ull * m, o_ord = o_len + 4ull * m, o_end = align8(o_ord + 4ull * m);
         const uint64_t o_dig = o_end;
-        HIP_TRY(c, sl.stage.ensure(o_end));
-        HIP_TRY(c, sl.dev.ensure(o_dig + 32ull * std::max<uint32_t>(m, 1)));
-        uint8_t* st = sl.stage.as<uint8_t>();
+        HIP_TRY(c, stage.ensure(o_end));
+        HIP_TRY(c, dev.ensure(o_dig + 32ull * std::max<uint32_t>(m, 1)));
+        uint8_t* st = stage.as<uint8_t>();
         mirsha::host::pack(slice_ptr, slice_len, slice_first, ids, m, poff.data(), st,
                            mirsha::host::threads_for(bytes, m));
         memcpy(st + o_off, poff.data(), 8ull * m);
         memcpy(st + o_len, plen.data(), 4ull * m);
         const bool identity = bucket_order(plen.data(), m, reinterpret_cast<uint32_t*>(st + o_ord));
-        uint8_t* dv = sl.dev.as<uint8_t>();
+        uint8_t* dv = dev.as<uint8_t>();
         if (m) {
             HIP_TRY(c, hipMemcpyAsync(dv, st, o_end, hipMemcpyHostToDevice, c->stream));
             int rc = timed_launch(c, 0, [&] {
@@ -1507,34 +1493,60 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
             HIP_TRY(c, hipMemcpyAsync(sl.dig.as<uint8_t>() + 32ull * row0, dv + o_dig, 32ull * m,
                                       hipMemcpyDeviceToHost, c->stream));
         }
+        ph[MIRSHA_PROF_PACK] += ms_since(tq);
         return MIRSHA_OK;
     };
-    uint32_t m = dedup ? (uint32_t)which.size() : n;
-    if (int rc = queue(dedup ? which.data() : nullptr, m, 0)) return rc;
-    ph[MIRSHA_PROF_PACK] = ms_since(t0);
-    sl.t_queued = Clock::now();
-    if (dedup) {
+    uint32_t m = n;
+    if (!dedup) {
+        if (int rc = queue(nullptr, n, 0, sl.stage, sl.dev)) return rc;
+        sl.t_queued = Clock::now();
+    } else {
+        mirsha::host::DedupScan d(slice_ptr, slice_len, slice_first, n, MIRSHA_MAX_MESSAGE_BYTES);
+        const std::vector<uint32_t> seg = d.segments();
+        std::vector<uint32_t> first_heads, later;  // the first launch's rows, then the second's
+        bool queued = false;
+        for (size_t k = 0; k + 1 < seg.size(); k++) {
+            const uint32_t lo = seg[k], hi = seg[k + 1];
+            t0 = Clock::now();
+            const bool ok = d.scan(lo, hi);
+            ph[MIRSHA_PROF_VALIDATE] += ms_since(t0);
+            if (!ok) {
+                // the first launch still reads this slot's buffers: let it finish
+                if (queued) HIP_TRY(c, hipStreamSynchronize(c->stream));
+                return slice_errors(c, d.err(), n);
+            }
+            t0 = Clock::now();
+            for (uint32_t i = lo; i < hi; i++) len[i] = (uint32_t)d.req_len()[i];
+            d.assign(lo, hi, k == 0 ? first_heads : later);
+            ph[MIRSHA_PROF_PLAN] += ms_since(t0);
+            if (k == 0) {
+                if (int rc = queue(first_heads.data(), (uint32_t)first_heads.size(), 0, sl.stage, sl.dev))
+                    return rc;
+                queued = true;
+                sl.t_queued = Clock::now();
+            }
+            t0 = Clock::now();
+            d.confirm(lo, hi);
+            ph[MIRSHA_PROF_PLAN] += ms_since(t0);
+        }
         t0 = Clock::now();
         std::vector<uint32_t> rep(n);
-        const uint32_t distinct = mirsha::host::dedup_resolve(slice_ptr, slice_len, slice_first, n, rl.data(),
-                                                              fp.data(), tent.data(), rep.data());
+        const uint32_t distinct = d.resolve(rep.data(), &later);  // collisions appended to `later`
+        const uint32_t m0 = (uint32_t)first_heads.size();
+        m = m0 + (uint32_t)later.size();
+        if (m != distinct) return fail(c, MIRSHA_EHIP, "dedup: %u representatives for %u contents", m, distinct);
         sl.rank.resize(n);
-        for (uint32_t k = 0; k < m; k++) sl.rank[which[k]] = k;
-        const bool heads_only = distinct == m;
-        if (distinct > m) {  // collided requests that are representatives of their own
-            std::vector<uint32_t> extra;
-            for (uint32_t i = 0; i < n; i++)
-                if (rep[i] == i && tent[i] != i) {
-                    sl.rank[i] = m + (uint32_t)extra.size();
-                    extra.push_back(i);
-                }
-            HIP_TRY(c, hipStreamSynchronize(c->stream));  // the first launch's staging buffers are reused
-            if (int rc = queue(extra.data(), (uint32_t)extra.size(), m)) return rc;
-            m += (uint32_t)extra.size();
+        for (uint32_t k = 0; k < m0; k++) sl.rank[first_heads[k]] = k;
+        for (uint32_t k = 0; k < (uint32_t)later.size(); k++) sl.rank[later[k]] = m0 + k;
+        bool identity = true;
+        for (uint32_t i = 0; i < n; i++) {
+            sl.rank[i] = sl.rank[rep[i]];
+            identity &= sl.rank[i] == i;
         }
-        for (uint32_t i = 0; i < n; i++) sl.rank[i] = sl.rank[rep[i]];
-        if (heads_only && m == n) sl.rank.clear();  // all distinct: rows are already in origin order
+        if (identity) sl.rank.clear();  // all distinct, rows already in origin order
         ph[MIRSHA_PROF_PLAN] += ms_since(t0);
+        if (!later.empty())
+            if (int rc = queue(later.data(), (uint32_t)later.size(), m0, sl.stage2, sl.dev2)) return rc;
     }
     if (n_unique_out) *n_unique_out = m;
     HIP_TRY(c, hipEventRecord(sl.done, c->stream));
@@ -1610,7 +1622,7 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     if (c->xin) (void)hipStreamDestroy(c->xin);
     if (c->xout) (void)hipStreamDestroy(c->xout);
     for (auto& sl : c->slots) {
-        sl.stage.release(); sl.dig.release(); sl.dev.release();
+        sl.stage.release(); sl.dig.release(); sl.dev.release(); sl.stage2.release(); sl.dev2.release();
         if (sl.done) (void)hipEventDestroy(sl.done);
     }
     if (c->own) (void)hipStreamDestroy(c->own);

@@ -279,41 +279,64 @@ bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, u
 }
 
 namespace {
-// Tentative representative: first request with the same (fingerprint, length).
-uint32_t assign_heads(uint32_t n, const uint64_t* req_len, const uint64_t* fp, uint32_t* tent) {
-    std::unordered_map<uint64_t, uint32_t> head;
-    head.reserve((size_t)n * 2);
-    uint32_t heads = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint64_t key = fp[i] ^ (req_len[i] * 0x9E3779B97F4A7C15ull);
-        auto it = head.emplace(key, i).first;
-        tent[i] = it->second;
-        heads += tent[i] == i;
-    }
-    return heads;
+inline uint64_t dedup_key(uint64_t fp, uint64_t len) { return fp ^ (len * 0x9E3779B97F4A7C15ull); }
+
+// Test hook (with MIRSHA_AB=1): slices per segment, so that small test inputs
+// run the multi-segment path.
+uint64_t env_segment_slices() {
+    static const uint64_t v = [] {
+        const char* ab = getenv("MIRSHA_AB");
+        const char* e = getenv("MIRSHA_DEDUP_SEGMENT_SLICES");
+        return ab && ab[0] == '1' && e ? strtoull(e, nullptr, 10) : 0ull;
+    }();
+    return v;
 }
 }  // namespace
 
-bool dedup_candidates_checked(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                              uint32_t ns, uint64_t max_len, uint64_t* req_len, uint8_t* err, uint64_t* fp,
-                              uint32_t* tent, uint32_t* heads) {
-    *heads = 0;
-    if (n == 0) return true;
+DedupScan::DedupScan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+                     uint64_t max_len)
+    : ptr_(ptr), len_(len), first_(first), n_(n), ns_(n ? first[n] : 0u), max_len_(max_len), req_len_(n, 0),
+      fp_(n, 0), tent_(n, kUnset), err_(n, 0), ok_(n, 0) {
+    head_.reserve((size_t)std::min<uint32_t>(n, 1u << 16) * 2);
+}
+
+std::vector<uint32_t> DedupScan::segments() const {
+    // ~1/16 of the slice arrays per segment (config 4: 256 acks = 15.8 MB of
+    // payload + 15.8 MB of slice arrays), at least 2^18 slices; a call below
+    // 2^19 slices is one segment (the plain two-pass plan).
+    uint64_t per = env_segment_slices();
+    if (!per) per = ns_ < (1u << 19) ? ~0ull : std::max<uint64_t>(ns_ / 16u, 1u << 18);
+    std::vector<uint32_t> b{0u};
+    uint64_t next = per;
+    for (uint32_t i = 1; i < n_; i++) {
+        // first[] may be malformed here (scan reports it); cut only where it is monotone
+        if (first_[i] >= next && first_[i] <= ns_ && first_[i] >= first_[b.back()]) {
+            b.push_back(i);
+            next = (uint64_t)first_[i] + per;
+        }
+    }
+    b.push_back(n_);
+    return b;
+}
+
+bool DedupScan::scan(uint32_t lo, uint32_t hi) {
+    if (lo >= hi) return true;
     const bool weak = weak_fp();
     std::atomic<bool> bad{false};
-    parallel_for(n, threads_for(16ull * ns, n), [&](uint32_t lo, uint32_t hi) {
-        for (uint32_t i = lo; i < hi; i++) {
-            err[i] = 0;
-            req_len[i] = 0;
-            fp[i] = 0;
-            if (first[i + 1] < first[i] || first[i + 1] > ns) { err[i] = 1; bad = true; continue; }
+    const uint64_t meta = 16ull * ((first_[hi] > first_[lo] && first_[hi] <= ns_) ? first_[hi] - first_[lo] : 0u);
+    parallel_for(hi - lo, threads_for(meta, hi - lo), [&](uint32_t a, uint32_t b) {
+        for (uint32_t i = lo + a; i < lo + b; i++) {
+            err_[i] = 0;
+            req_len_[i] = 0;
+            fp_[i] = 0;
+            if (first_[i + 1] < first_[i] || first_[i + 1] > ns_) { err_[i] = 1; bad = true; continue; }
             Fp f;
             bool over = false;  // past max_len: no more bytes read (as slice_lengths, which reads none)
-            for (uint32_t s = first[i]; s < first[i + 1]; s++) {
-                const uint64_t L = len[s];
-                const uint8_t* p = ptr[s];
-                if (L && !p) { err[i] = 2; break; }
-                if (!over && f.total + L > max_len) over = true;
+            for (uint32_t s = first_[i]; s < first_[i + 1]; s++) {
+                const uint64_t L = len_[s];
+                const uint8_t* p = ptr_[s];
+                if (L && !p) { err_[i] = 2; break; }
+                if (!over && f.total + L > max_len_) over = true;
                 if (weak || over) { f.total += L; continue; }
                 if (f.nc == 0 && L == 8) {  // as fingerprint(): whole words at a word boundary
                     uint64_t w;
@@ -327,63 +350,80 @@ bool dedup_candidates_checked(const uint8_t* const* ptr, const uint64_t* len, co
                     f.bytes(p, L);
                 }
             }
-            if (!err[i] && f.total > max_len) err[i] = 3;
-            if (err[i]) { bad = true; continue; }
-            req_len[i] = f.total;
-            fp[i] = weak ? 0 : f.final();
+            if (!err_[i] && f.total > max_len_) err_[i] = 3;
+            if (err_[i]) { bad = true; continue; }
+            req_len_[i] = f.total;
+            fp_[i] = weak ? 0 : f.final();
+            // A head from an earlier segment (the table is read-only while
+            // segments are scanned): confirm now, while this request's bytes
+            // and slice arrays are still in this core's cache.
+            const auto it = head_.find(dedup_key(fp_[i], f.total));
+            if (it != head_.end()) {
+                const uint32_t j = it->second;
+                tent_[i] = j;
+                ok_[i] = req_len_[j] == f.total &&
+                         equal_concat(ptr_, len_, first_[i], first_[i + 1], first_[j], first_[j + 1]);
+            }
         }
     });
-    if (bad) return false;
-    *heads = assign_heads(n, req_len, fp, tent);
-    return true;
+    return !bad;
 }
 
-uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                          const uint64_t* req_len, uint64_t* fp, uint32_t* tent) {
-    if (n == 0) return 0;
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; i++) total += req_len[i];
-    parallel_for(n, threads_for(total, n), [&](uint32_t lo, uint32_t hi) {
-        for (uint32_t i = lo; i < hi; i++) fp[i] = fingerprint(ptr, len, first[i], first[i + 1]);
-    });
-    return assign_heads(n, req_len, fp, tent);
+void DedupScan::assign(uint32_t lo, uint32_t hi, std::vector<uint32_t>& heads) {
+    for (uint32_t i = lo; i < hi; i++) {
+        if (tent_[i] != kUnset) continue;  // matched a head of an earlier segment in scan()
+        const auto it = head_.emplace(dedup_key(fp_[i], req_len_[i]), i).first;
+        tent_[i] = it->second;
+        if (tent_[i] == i) {
+            ok_[i] = 1;
+            heads.push_back(i);
+        } else {
+            ok_[i] = kPending;
+        }
+    }
 }
 
-uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                       const uint64_t* req_len, const uint64_t* fp, const uint32_t* tent, uint32_t* rep) {
-    if (n == 0) return 0;
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; i++) total += req_len[i];
-    // Confirm byte for byte (in parallel); a mismatch is a fingerprint collision.
-    std::vector<uint8_t> ok(n, 1);
-    parallel_for(n, threads_for(total, n), [&](uint32_t lo, uint32_t hi) {
-        for (uint32_t i = lo; i < hi; i++) {
-            const uint32_t j = tent[i];
-            if (j != i)
-                ok[i] = req_len[i] == req_len[j] &&
-                        equal_concat(ptr, len, first[i], first[i + 1], first[j], first[j + 1]);
+void DedupScan::confirm(uint32_t lo, uint32_t hi) {
+    if (lo >= hi) return;
+    uint64_t bytes = 0;
+    uint32_t m = 0;
+    for (uint32_t i = lo; i < hi; i++)
+        if (ok_[i] == kPending) {
+            bytes += req_len_[i];
+            m++;
+        }
+    if (!m) return;
+    parallel_for(hi - lo, threads_for(bytes, m), [&](uint32_t a, uint32_t b) {
+        for (uint32_t i = lo + a; i < lo + b; i++) {
+            if (ok_[i] != kPending) continue;
+            const uint32_t j = tent_[i];
+            ok_[i] = req_len_[i] == req_len_[j] &&
+                     equal_concat(ptr_, len_, first_[i], first_[i + 1], first_[j], first_[j + 1]);
         }
     });
-    // Sequential resolution: confirmed -> tentative rep; collided -> search the
-    // distinct representatives already seen under this key (rare).
+}
+
+uint32_t DedupScan::resolve(uint32_t* rep, std::vector<uint32_t>* extra) {
+    // Sequential: confirmed -> tentative rep; collided -> search the distinct
+    // representatives already seen under this key (rare).
     std::unordered_map<uint64_t, std::vector<uint32_t>> reps;  // only keys that collided
     uint32_t distinct = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint32_t j = tent[i];
+    for (uint32_t i = 0; i < n_; i++) {
+        const uint32_t j = tent_[i];
         if (j == i) {
             rep[i] = i;
             distinct++;
             continue;
         }
-        if (ok[i]) {
+        if (ok_[i] == 1) {
             rep[i] = j;
             continue;
         }
-        const uint64_t key = fp[i] ^ (req_len[i] * 0x9E3779B97F4A7C15ull);
-        auto& cand = reps[key];
+        auto& cand = reps[dedup_key(fp_[i], req_len_[i])];
         uint32_t found = UINT32_MAX;
         for (uint32_t r : cand)
-            if (req_len[r] == req_len[i] && equal_concat(ptr, len, first[i], first[i + 1], first[r], first[r + 1])) {
+            if (req_len_[r] == req_len_[i] &&
+                equal_concat(ptr_, len_, first_[i], first_[i + 1], first_[r], first_[r + 1])) {
                 found = r;
                 break;
             }
@@ -391,6 +431,7 @@ uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uin
             cand.push_back(i);
             rep[i] = i;
             distinct++;
+            if (extra) extra->push_back(i);
         } else {
             rep[i] = found;
         }
@@ -402,12 +443,20 @@ uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uin
 }
 
 uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                    const uint64_t* req_len, uint32_t* rep) {
-    if (n == 0) return 0;
-    std::vector<uint64_t> fp(n);
-    std::vector<uint32_t> tent(n);
-    dedup_candidates(ptr, len, first, n, req_len, fp.data(), tent.data());
-    return dedup_resolve(ptr, len, first, n, req_len, fp.data(), tent.data(), rep);
+                    uint32_t* rep, const uint8_t** err_out, std::vector<uint8_t>* err) {
+    DedupScan d(ptr, len, first, n, ~0ull);
+    const std::vector<uint32_t> seg = d.segments();
+    std::vector<uint32_t> heads;
+    for (size_t k = 0; k + 1 < seg.size(); k++) {
+        if (!d.scan(seg[k], seg[k + 1])) {
+            if (err) err->assign(d.err(), d.err() + n);
+            if (err_out) *err_out = err ? err->data() : nullptr;
+            return UINT32_MAX;
+        }
+        d.assign(seg[k], seg[k + 1], heads);
+        d.confirm(seg[k], seg[k + 1]);
+    }
+    return d.resolve(rep, nullptr);
 }
 
 void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,
@@ -473,19 +522,9 @@ extern "C" int mirsha_dedup_plan(const uint8_t* const* slice_ptr, const uint64_t
         return MIRSHA_OK;
     }
     if (!slice_first || !rep_out || slice_first[0] != 0) return MIRSHA_EINVAL;
-    const uint32_t ns = slice_first[n];
-    if (ns && (!slice_ptr || !slice_len)) return MIRSHA_EINVAL;
-    std::vector<uint64_t> req_len(n);
-    for (uint32_t i = 0; i < n; i++) {
-        if (slice_first[i + 1] < slice_first[i]) return MIRSHA_EINVAL;
-        uint64_t L = 0;
-        for (uint32_t s = slice_first[i]; s < slice_first[i + 1]; s++) {
-            if (slice_len[s] && !slice_ptr[s]) return MIRSHA_EINVAL;
-            L += slice_len[s];
-        }
-        req_len[i] = L;
-    }
-    const uint32_t u = mirsha::host::dedup_plan(slice_ptr, slice_len, slice_first, n, req_len.data(), rep_out);
+    if (slice_first[n] && (!slice_ptr || !slice_len)) return MIRSHA_EINVAL;
+    const uint32_t u = mirsha::host::dedup_plan(slice_ptr, slice_len, slice_first, n, rep_out, nullptr, nullptr);
+    if (u == UINT32_MAX) return MIRSHA_EINVAL;  // slice_first not monotone / a NULL slice with bytes
     if (n_unique_out) *n_unique_out = u;
     return MIRSHA_OK;
 }

@@ -12,6 +12,8 @@
 #include <stdint.h>
 
 #include <functional>
+#include <unordered_map>
+#include <vector>
 
 namespace mirsha {
 namespace host {
@@ -34,32 +36,60 @@ uint64_t fingerprint(const uint8_t* const* ptr, const uint64_t* len, uint32_t s0
 bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, uint32_t a1, uint32_t b0,
                   uint32_t b1);
 
-// rep[i] = the smallest j <= i whose request bytes equal request i's (i if
-// none).  req_len[i] = total bytes of request i.  Returns the number of
-// distinct requests (rep[i] == i).  = dedup_candidates + dedup_resolve.
+// Content-addressed dedup of n requests (slice lists), streamed over
+// contiguous request ranges ("segments") in origin order, so the caller can
+// start hashing the first segment's distinct requests while the rest is still
+// being scanned:
+//   for each segment [lo, hi):  scan(lo, hi); assign(lo, hi, heads); confirm(lo, hi);
+//   then resolve(rep, &extra).
+// scan: validation + a slicing-independent 64-bit fingerprint per request
+// (one walk over its slice arrays, in parallel); a request whose
+// (fingerprint, length) key matches a head of an EARLIER segment is compared
+// with it byte for byte right there, while its bytes are cache-warm.
+// assign: the remaining requests of the segment in origin order; the first
+// request of a new key is a head (appended to `heads`): every head is a final
+// representative, so it may be hashed at once.
+// confirm: byte comparison of the segment's other tentative matches.
+// resolve: rep[i] = the smallest j <= i whose bytes equal request i's (i if
+// none); fingerprint collisions (a key match that the bytes refute, rare)
+// become representatives too and are appended to `extra`.  Returns the number
+// of distinct requests.  Equality is never decided by the fingerprint.
+class DedupScan {
+  public:
+    DedupScan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
+              uint64_t max_len);
+    // Segment boundaries b[0] = 0 < ... < b.back() = n (~1/16 of the slices
+    // each; one segment for small calls).
+    std::vector<uint32_t> segments() const;
+    // False if any request of [lo, hi) is malformed: err()[i] = 1 slice_first
+    // not monotone or past its end, 2 a NULL slice with bytes, 3 longer than
+    // max_len.
+    bool scan(uint32_t lo, uint32_t hi);
+    void assign(uint32_t lo, uint32_t hi, std::vector<uint32_t>& heads);
+    void confirm(uint32_t lo, uint32_t hi);
+    uint32_t resolve(uint32_t* rep, std::vector<uint32_t>* extra);
+    const uint64_t* req_len() const { return req_len_.data(); }
+    const uint8_t* err() const { return err_.data(); }
+
+  private:
+    static constexpr uint32_t kUnset = 0xFFFFFFFFu;
+    static constexpr uint8_t kPending = 2;  // ok_: 0 refuted, 1 confirmed (or a head), 2 to confirm
+    const uint8_t* const* ptr_;
+    const uint64_t* len_;
+    const uint32_t* first_;
+    uint32_t n_, ns_;
+    uint64_t max_len_;
+    std::vector<uint64_t> req_len_, fp_;
+    std::vector<uint32_t> tent_;
+    std::vector<uint8_t> err_, ok_;
+    std::unordered_map<uint64_t, uint32_t> head_;
+};
+
+// The whole plan on the host (mirsha_dedup_plan): rep[] as DedupScan::resolve;
+// returns the distinct count, or UINT32_MAX on malformed slice arrays (then
+// *err_out = per-request codes if `err` is given).
 uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                    const uint64_t* req_len, uint32_t* rep);
-
-// First half of dedup_plan: fingerprints fp[i] and tentative representatives
-// tent[i] = the first request with the same (fingerprint, length).  Returns
-// the number of heads (tent[i] == i); every head is a final representative,
-// so their hashing may start before dedup_resolve confirms the rest.
-uint32_t dedup_candidates(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                          const uint64_t* req_len, uint64_t* fp, uint32_t* tent);
-
-// dedup_candidates with the call's slice validation folded into the same walk
-// over the slice arrays (config 4: 15.7 M slices of 8-32 B, so the arrays are
-// as large as the payload): per request its length req_len[i] and err[i]
-// (0 ok, 1 slice_first not monotone or past ns, 2 a NULL slice with bytes,
-// 3 longer than max_len).  Returns false (tent unset) if any err[i] != 0.
-bool dedup_candidates_checked(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                              uint32_t ns, uint64_t max_len, uint64_t* req_len, uint8_t* err, uint64_t* fp,
-                              uint32_t* tent, uint32_t* heads);
-
-// Second half: confirms every tentative match byte for byte and resolves
-// fingerprint collisions; fills rep[] as dedup_plan.  Returns distinct count.
-uint32_t dedup_resolve(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                       const uint64_t* req_len, const uint64_t* fp, const uint32_t* tent, uint32_t* rep);
+                    uint32_t* rep, const uint8_t** err_out, std::vector<uint8_t>* err);
 
 // Copies request which[k] (k < m) to dst + dst_off[k], in parallel.
 void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,

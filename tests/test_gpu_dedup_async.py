@@ -199,12 +199,20 @@ def test_dropped_ticket_then_four_more(engine):
     assert not engine._outstanding
 
 
-def test_dedup_collision_path_second_launch():
-    """MIRSHA_DEDUP_WEAK_FP=1 (read once per process, hence a subprocess):
-    every fingerprint is equal, so the heads queued before the byte-for-byte
-    confirmation are only one request per length, and every other distinct
-    request is found by the confirmation and hashed in the second launch.
-    Digests in origin order, dedup count exact, sync and async forms."""
+@pytest.mark.parametrize("knobs", [{"MIRSHA_DEDUP_WEAK_FP": "1"},
+                                   {"MIRSHA_DEDUP_SEGMENT_SLICES": "40"},
+                                   {"MIRSHA_DEDUP_WEAK_FP": "1", "MIRSHA_DEDUP_SEGMENT_SLICES": "40"}])
+def test_dedup_collision_path_second_launch(knobs):
+    """Test hooks read once per process, hence a subprocess.
+    MIRSHA_DEDUP_WEAK_FP=1: every fingerprint is equal, so the heads queued
+    before the byte-for-byte confirmation are only one request per length, and
+    every other distinct request is found by the confirmation and hashed in
+    the second launch.  MIRSHA_DEDUP_SEGMENT_SLICES=40: the streamed scan in
+    segments of ~40 slices, the first segment's heads launched before the rest
+    is scanned, later heads in the second launch; a malformed request in a
+    later segment (after the first launch was queued) fails the call and the
+    context hashes on.  Digests in origin order, dedup count exact, sync and
+    async forms."""
     import os
     import subprocess
     import sys
@@ -224,10 +232,21 @@ def test_dedup_collision_path_second_launch():
         "    assert e.last_unique == t.python_plan(reqs)[1], seed\n"
         "    tk = e.submit_slices(reqs, dedup=True)\n"
         "    assert [r.tobytes() for r in e.wait(tk)] == want, seed\n"
+        "from mirbft_amd import SliceArrays\n"
+        "from mirbft_amd._lib import MirshaError\n"
+        "sl = SliceArrays.from_requests([[bytes([i % 7]) * 70, b'c'] for i in range(60)])\n"
+        "sl.ptr[101] = 0\n"
+        "try:\n"
+        "    e.hash_slice_arrays(sl, dedup=True)\n"
+        "    raise SystemExit('no error')\n"
+        "except MirshaError as x:\n"
+        "    assert 'request 50' in str(x), str(x)\n"
+        "ok = [[b'abc', b'def'], [b'abcdef'], [b'xyz']]\n"
+        "assert [r.tobytes() for r in e.hash_slices(ok, dedup=True)] == [hashlib.sha256(b''.join(r)).digest() for r in ok]\n"
         "e.close()\n"
         "print('ok')\n" % (root, os.path.join(root, "tests"))
     )
-    env = dict(os.environ, MIRSHA_AB="1", MIRSHA_DEDUP_WEAK_FP="1")
+    env = dict(os.environ, MIRSHA_AB="1", **knobs)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 

@@ -87,6 +87,36 @@ def test_weak_fingerprint_collisions_resolved_exactly():
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr
 
 
+@pytest.mark.parametrize("weak", ["0", "1"])
+def test_streamed_segments(weak):
+    """The scan in segments of a few slices (test hook MIRSHA_DEDUP_SEGMENT_SLICES,
+    read once per process, hence a subprocess): heads of later segments,
+    matches confirmed inside the scan against heads of earlier segments, and
+    (weak fingerprints) collisions across segments all give the plan of the
+    one-segment scan; a malformed request in a later segment is still found."""
+    code = (
+        "import sys, ctypes; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+        "import numpy as np\n"
+        "import test_host_dedup as t\n"
+        "from mirbft_amd import dedup_plan, SliceArrays, _lib\n"
+        "for seed in (0, 1, 2, 3):\n"
+        "    reqs = t.random_requests(seed, n=200)\n"
+        "    rep, u = dedup_plan(reqs)\n"
+        "    want, wu = t.python_plan(reqs)\n"
+        "    assert rep.tolist() == want.tolist() and u == wu, seed\n"
+        "sl = SliceArrays.from_requests([[b'ab', b'c']] * 30)\n"
+        "ptr = sl.ptr.copy(); ptr[47] = 0\n"
+        "rep = np.zeros(30, dtype=np.uint32); u = ctypes.c_uint32(0)\n"
+        "rc = _lib.load().mirsha_dedup_plan(ptr.ctypes.data, sl.len.ctypes.data, sl.first.ctypes.data, 30,\n"
+        "                                   rep.ctypes.data, ctypes.byref(u))\n"
+        "assert rc == _lib.MIRSHA_EINVAL, rc\n"
+        "print('ok')\n" % (ROOT, os.path.join(ROOT, "tests"))
+    )
+    env = dict(os.environ, MIRSHA_AB="1", MIRSHA_DEDUP_SEGMENT_SLICES="5", MIRSHA_DEDUP_WEAK_FP=weak)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr
+
+
 def test_epoch_change_cycle_parallel_pass():
     """Config-4 shape (acks of every origin relayed by every source), large
     enough (> 4 MiB) for the multi-threaded fingerprint / confirm passes."""
