@@ -293,6 +293,41 @@ uint64_t env_segment_slices() {
 }
 }  // namespace
 
+namespace {
+// Key of a request's first min(64, L) bytes (slicing-independent): the
+// speculation key of DedupScan::scan.  False if a slice with bytes has no
+// address (the request is malformed; the fingerprint walk reports it).
+bool prefix_key(const uint8_t* const* ptr, const uint64_t* len, uint32_t s0, uint32_t s1, uint64_t* key) {
+    uint8_t buf[64];
+    uint32_t got = 0;
+    for (uint32_t s = s0; s < s1 && got < 64u; s++) {
+        const uint64_t L = len[s];
+        if (!L) continue;
+        if (!ptr[s]) return false;
+        const uint32_t k = (uint32_t)std::min<uint64_t>(L, 64u - got);
+        memcpy(buf + got, ptr[s], k);
+        got += k;
+    }
+    memset(buf + got, 0, 64u - got);
+    Fp f;
+    f.total = got;
+    f.words4(buf);
+    f.words4(buf + 32);
+    *key = f.final();
+    return true;
+}
+
+// equal_concat for a request `a` that is not validated yet: false (not equal)
+// as soon as one of its slices with bytes has no address, and no byte of `a`
+// past b's length is read.
+bool equal_concat_checked(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, uint32_t a1, uint32_t b0,
+                          uint32_t b1) {
+    for (uint32_t s = a0; s < a1; s++)
+        if (len[s] && !ptr[s]) return false;
+    return equal_concat(ptr, len, a0, a1, b0, b1);
+}
+}  // namespace
+
 DedupScan::DedupScan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
                      uint64_t max_len)
     : ptr_(ptr), len_(len), first_(first), n_(n), ns_(n ? first[n] : 0u), max_len_(max_len), req_len_(n, 0),
@@ -330,6 +365,29 @@ bool DedupScan::scan(uint32_t lo, uint32_t hi) {
             req_len_[i] = 0;
             fp_[i] = 0;
             if (first_[i + 1] < first_[i] || first_[i + 1] > ns_) { err_[i] = 1; bad = true; continue; }
+            // Speculation: the head of an earlier segment with the same first
+            // 64 bytes.  Equal bytes (one walk, compared slice by slice) make
+            // the fingerprint walk unnecessary: equal contents have equal
+            // lengths and fingerprints, and that head is the first request with
+            // this content (heads are the first of their (fingerprint, length)
+            // key).  A refuted guess costs the comparison up to the first
+            // difference, then the request takes the fingerprint walk.
+            if (!prefix_.empty()) {
+                uint64_t pk;
+                if (prefix_key(ptr_, len_, first_[i], first_[i + 1], &pk)) {
+                    const auto it = prefix_.find(pk);
+                    if (it != prefix_.end()) {
+                        const uint32_t j = it->second;
+                        if (equal_concat_checked(ptr_, len_, first_[i], first_[i + 1], first_[j], first_[j + 1])) {
+                            req_len_[i] = req_len_[j];
+                            fp_[i] = fp_[j];
+                            tent_[i] = j;
+                            ok_[i] = 1;
+                            continue;
+                        }
+                    }
+                }
+            }
             Fp f;
             bool over = false;  // past max_len: no more bytes read (as slice_lengths, which reads none)
             for (uint32_t s = first_[i]; s < first_[i + 1]; s++) {
@@ -377,6 +435,8 @@ void DedupScan::assign(uint32_t lo, uint32_t hi, std::vector<uint32_t>& heads) {
         if (tent_[i] == i) {
             ok_[i] = 1;
             heads.push_back(i);
+            uint64_t pk;
+            if (prefix_key(ptr_, len_, first_[i], first_[i + 1], &pk)) prefix_.emplace(pk, i);
         } else {
             ok_[i] = kPending;
         }

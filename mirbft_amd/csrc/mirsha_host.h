@@ -45,7 +45,9 @@ bool equal_concat(const uint8_t* const* ptr, const uint64_t* len, uint32_t a0, u
 // scan: validation + a slicing-independent 64-bit fingerprint per request
 // (one walk over its slice arrays, in parallel); a request whose
 // (fingerprint, length) key matches a head of an EARLIER segment is compared
-// with it byte for byte right there, while its bytes are cache-warm.
+// with it byte for byte right there, while its bytes are cache-warm.  A
+// request whose first 64 bytes match such a head is compared with it first:
+// if equal, that one walk settles it (no fingerprint walk).
 // assign: the remaining requests of the segment in origin order; the first
 // request of a new key is a head (appended to `heads`): every head is a final
 // representative, so it may be hashed at once.
@@ -83,6 +85,7 @@ class DedupScan {
     std::vector<uint32_t> tent_;
     std::vector<uint8_t> err_, ok_;
     std::unordered_map<uint64_t, uint32_t> head_;
+    std::unordered_map<uint64_t, uint32_t> prefix_;  // first 64 bytes -> the first head with them
 };
 
 // The whole plan on the host (mirsha_dedup_plan): rep[] as DedupScan::resolve;
