@@ -234,7 +234,7 @@ def test_dedup_collision_path_second_launch(knobs):
         "    assert [r.tobytes() for r in e.wait(tk)] == want, seed\n"
         "from mirbft_amd import SliceArrays\n"
         "from mirbft_amd._lib import MirshaError\n"
-        "sl = SliceArrays.from_requests([[bytes([i % 7]) * 70, b'c'] for i in range(60)])\n"
+        "sl = SliceArrays.from_requests([[bytes([i & 7]) * 70, b'c'] for i in range(60)])\n"
         "sl.ptr[101] = 0\n"
         "try:\n"
         "    e.hash_slice_arrays(sl, dedup=True)\n"
