@@ -175,10 +175,15 @@ int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
 
 /* Host-side phases (milliseconds) of the context's last host-API call.
  * Slice submissions (mirsha_submit_slices / mirsha_hash_slices_dedup):
- * validate = slice lengths; plan = dedup plan (fingerprint + byte-for-byte
- * confirm); pack = gather into pinned staging + bucket order; device = queued
- * -> complete (H2D, kernel, D2H, plus any time the caller spent before
- * waiting); scatter = digests copied to the caller in origin order.
+ * validate = slice lengths (dedup: the segmented scan -- validation plus a
+ * fingerprint walk or a byte comparison per request); plan = dedup plan
+ * (head assignment, the remaining byte-for-byte confirmations, resolution);
+ * pack = gather into pinned staging + bucket order + queueing, over every
+ * launch (dedup: the first segment's distinct requests are queued before the
+ * rest is scanned, later ones in a second launch); device = first launch
+ * queued -> complete (H2D, kernels, D2H, overlapping the dedup scan of the
+ * later segments and any time the caller spent before waiting); scatter =
+ * digests copied to the caller in origin order.
  * Synchronous calls (mirsha_hash_batch / _slices / _requests_then_batches /
  * mirsha_digest_lists): validate = arguments; pack = queueing the request
  * bytes (pinned arena: one DMA; else packing into pinned chunks behind their

@@ -1270,8 +1270,13 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.seg_per_tile = p->seg_per_tile;
     a.seg_nominal_nb = p->seg_nominal_nb;
     a.seg_epoch = p->seg_runs;
-    a.tile_prio_progress = overlap ? 1u : 0u;
-    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_OVERLAP_QUEUE_PRIO")) a.tile_prio_progress = overlap && e[0] != '1';
+    // Overlapped cycles: no chain waits on these tiles, so no queue order to
+    // keep: the SIMD's tile waves at priorities by progress rank (kPrioBalance).
+    // A/B (MIRSHA_FUSED_OVERLAP_PRIO): queue = the fused launch's queue
+    // priorities, progress = the request kernel's progress_prio.
+    a.tile_prio_progress = overlap ? 2u : 0u;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_OVERLAP_PRIO"))
+        if (overlap) a.tile_prio_progress = strcmp(e, "queue") == 0 ? 0u : strcmp(e, "progress") == 0 ? 1u : 2u;
     a.seg_nb = p->d_seg_nb.as<uint32_t>();
     a.seg_state = p->d_seg_state.as<uint32_t>();
     a.seg_flags = p->d_seg_flags.as<unsigned long long>();

@@ -24,7 +24,7 @@ enum : int {
 };
 inline bool variant_valid(int v) {
     return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair ||
-           v == kVariantCu || v == 11;
+           v == kVariantCu || v == 11 || v == 12;
 }
 constexpr uint32_t kCuMaxWavesPerSimd = 4;
 uint32_t cu_count();

@@ -234,6 +234,40 @@ __device__ __forceinline__ void fixed_prio(uint32_t p) {
     else __builtin_amdgcn_s_setprio(0);
 }
 
+// hash_tile<kFused>'s fprio: priority by rank of progress among the tile waves
+// of the SIMD (FusedArgs::tile_prio_progress == 2, overlapped cycles).  Each
+// wave publishes its block in its LDS word (bal[slot]; an idle or finished
+// wave's word is kBalDone) and, before each block, takes priority 3 minus the
+// number of the SIMD's waves it is ahead of: the wave furthest behind wins
+// issue.  With one fixed priority after a few blocks the arbiter's age order
+// ran the SIMD's waves one after another instead (config 3's overlapped
+// launch: waves ending at ~420 / 450 / 600 / 760 us, the last ~150 us at one
+// wave per SIMD, tools/trace_overlap.py); by rank they end together.
+constexpr uint32_t kPrioBalance = 5;
+constexpr uint32_t kBalDone = 0xFFFFFFFFu;
+// [SIMD][hardware wave slot] (HW_ID's SIMD_ID and WAVE_ID fields: read with
+// s_getreg where needed, so no register stays live across the block loop of
+// the fused kernel, which sits at its 128-VGPR budget).
+__shared__ uint32_t g_bal_prog[4 * 16];
+__device__ __forceinline__ uint32_t bal_word() {
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    return ((hw >> 4) & 3u) * 16u + (hw & 15u);
+}
+__device__ __forceinline__ void balance_prio(uint32_t blk) {
+    const uint32_t me = bal_word();
+    __hip_atomic_store(g_bal_prog + me, blk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t* row = g_bal_prog + (me & ~15u);
+    uint32_t ahead = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; k++)
+        ahead += __hip_atomic_load(row + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < blk ? 1u : 0u;
+    fixed_prio(3u - min(3u, (uint32_t)__builtin_amdgcn_readfirstlane((int)ahead)));
+}
+__device__ __forceinline__ void balance_done() {
+    __hip_atomic_store(g_bal_prog + bal_word(), kBalDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Software-pipelined block loop of a tile (kPf: launches of at most 4 waves
 // per SIMD, which leave a wave 128 VGPRs), for tiles whose messages are all
 // 4-byte aligned and whose loads all stay inside the arena.  Block b+1's
@@ -245,7 +279,7 @@ __device__ __forceinline__ void fixed_prio(uint32_t p) {
 // rounds: with 4 waves per SIMD started together (config 3) the waves reach
 // their staging at the same time and the one-at-a-time form left the SIMD
 // short of issuable waves there (643 us per config-3 launch, profiles/r03b).
-template <bool kNoYield>
+template <bool kNoYield, bool kBalance = false>
 __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc, const uint32_t vo[4],
                                                     const uint32_t sel[4], uint32_t L, uint32_t min_l, bool uni,
                                                     bool tail_ok, const TailWords& tw, uint32_t wave_nb,
@@ -308,7 +342,7 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
         pad_uniform(blk, w);
         const bool next = blk + 1u < wave_nb;  // wave-uniform
         uint32_t wn[16];
-        progress_prio(blk);
+        if constexpr (kBalance) balance_prio(blk); else progress_prio(blk);
         compress_asm_hooked<kNoYield>(st, w, blk < nb, [&](int k) {
             if (k == 0 && next) {
                 write_tile(blk + 1u);
@@ -323,7 +357,7 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
     if (tail_ok) {  // final block (<= 16 message bytes), staged during the loop's last block
         const uint32_t blk = wave_nb - 1u;
         pad_block_uniform<4>(w, 64u * blk, min_l, false);
-        progress_prio(blk);
+        if constexpr (kBalance) balance_prio(blk); else progress_prio(blk);
         if (blk < nb) compress_asm_tail(st, w, tw);
     }
 }
@@ -337,7 +371,7 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
 // [b0, b1) of the tile, from the midstate in st (H0 when b0 == 0).  Returns
 // true when the range reached the tile's end: the digest is then stored;
 // otherwise st holds the midstate after block b1 - 1.
-template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false>
+template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false, bool kBalance = false>
 __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
@@ -345,7 +379,9 @@ __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uin
                                           uint32_t b0 = 0u, uint32_t b1 = 0xFFFFFFFFu, uint32_t* st_io = nullptr) {
     auto block_prio = [&](uint32_t blk) {
         if constexpr (kFused) {
-            if (fprio == kPrioProgress)
+            if (fprio == kPrioBalance)
+                balance_prio(blk);
+            else if (fprio == kPrioProgress)
                 progress_prio(blk);
             else
                 fixed_prio(fprio);
@@ -503,8 +539,8 @@ __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uin
         const uint32_t loop_nb = tail_ok ? wave_nb - 1u : wave_nb;
         if constexpr (kPf) {
             if (far && aligned && b0 == 0u && finished) {
-                hash_tile_pipelined<kNoYield>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb, lane, my,
-                                              st);
+                hash_tile_pipelined<kNoYield, kBalance>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb,
+                                                        lane, my, st);
                 goto digest;
             }
         }
@@ -653,7 +689,7 @@ __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_ms
 // its SIMDs in cyclic order: exactly k waves per SIMD.  At k <= 4 a wave may
 // hold 128 VGPRs, so the next block's chunks are prefetched into registers.
 constexpr uint32_t kCuLds = 96u * 1024u;
-template <bool kNoYield>
+template <bool kNoYield, bool kBalance>
 __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* __restrict__ arena,
                                                                  uint64_t arena_len,
                                                                  const uint64_t* __restrict__ off,
@@ -664,9 +700,13 @@ __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * (blockDim.x >> 6) + wv;
+    if constexpr (kBalance) {
+        if (threadIdx.x < 64u) g_bal_prog[threadIdx.x] = kBalDone;
+        __syncthreads();
+    }
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<true, false, false, true, kNoYield>(arena, arena_len, off, len, order, n, out, cu_lds + 256u * wv, t,
-                                                  lane);
+    hash_tile<true, false, false, true, kNoYield, kBalance>(arena, arena_len, off, len, order, n, out,
+                                                            cu_lds + 256u * wv, t, lane);
 }
 
 // ---- overlapped cycles: this cycle's request tiles + the previous cycle's
@@ -1242,16 +1282,26 @@ __device__ __forceinline__ uint64_t claim(unsigned long long* ctr, uint32_t lane
     return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ void fused_retire(unsigned long long* ctl, uint32_t lane) {
+// Retire count per workgroup, not per wave: a wave counts itself in LDS and
+// the workgroup's last wave adds 1 to the device-scope word (adds on one word
+// serialise near 88 per us, MI355X_MICROARCH.md: the ~4,000 waves of a
+// balanced overlapped launch, ending within tens of us, queued behind each
+// other for their adds before they could end).  A workgroup's waves count
+// only after their claims returned, and its last wave adds only after every
+// wave of the workgroup counted, so the last add of the grid still follows
+// every claim of the run.
+__device__ __forceinline__ void fused_retire(unsigned long long* ctl, uint32_t lane, uint32_t* waves_retired) {
     if (lane != 0u) return;
-    const unsigned long long total = (unsigned long long)gridDim.x * (blockDim.x >> 6);
-    // Relaxed: every claim this wave made returned its value (the wave branched
-    // on it) before this add was issued, and device-scope atomics are
-    // performed at one point past the XCDs' L2s (an acq_rel add cost each of
-    // config 3's ~4,000 waves an L2 writeback: +70 us, profiles/r02ay).
+    const uint32_t waves = blockDim.x >> 6;
+    if (__hip_atomic_fetch_add(waves_retired, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1u != waves)
+        return;
+    // Relaxed: every claim returned its value (the wave branched on it)
+    // before the counts above, and device-scope atomics are performed at one
+    // point past the XCDs' L2s (an acq_rel add cost each of config 3's ~4,000
+    // waves an L2 writeback: +70 us, profiles/r02ay).
     const unsigned long long old =
         __hip_atomic_fetch_add(ctl + kCtlDone, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old + 1ull == total) {
+    if (old + 1ull == gridDim.x) {
         for (uint32_t q = 0; q < kFusedMaxQueues; q++)
             __hip_atomic_store(ctl + kCtlTileTicket + 16u * q, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(ctl + kCtlDone, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1525,11 +1575,14 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // (block-batched claims that tolerate any placement measured 12 us slower
     // per config-3 launch, profiles/r03l).
     __shared__ uint32_t simd_waves[4];
+    __shared__ uint32_t waves_retired;
     static_assert(kPacedRingOff + sizeof(FusedPairRing) <= kPacedLds && kPacedRingOff >= 4096u * kPacedMaxPace * 4u,
                   "paced LDS: staging tiles, then the pair ring");
     FusedPairRing& ring = *reinterpret_cast<FusedPairRing*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedRingOff);
     const bool list_block = blockIdx.x < a.list_waves;  // list_waves carries the number of LIST BLOCKS
     if (threadIdx.x < 4u) simd_waves[threadIdx.x] = 0u;
+    if (threadIdx.x == 0u) waves_retired = 0u;
+    if (threadIdx.x < 64u) g_bal_prog[threadIdx.x] = kBalDone;  // tile progress (kPrioBalance)
     if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = ring.aborted = 0u;
     __syncthreads();
     uint32_t hw;
@@ -1658,7 +1711,9 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             b1 = seg != kNoSeg ? seg_at : 0xFFFFFFFFu;
             // (overlapped cycles: no chain waits on these tiles, so no queue
             // order to keep -- the request kernel's progress priorities)
-            pr = a.tile_prio_progress ? kPrioProgress : prio_of(a.steal_own_prio ? q : qq, a.n_queues);
+            pr = a.tile_prio_progress == 2u ? kPrioBalance
+                 : a.tile_prio_progress     ? kPrioProgress
+                                            : prio_of(a.steal_own_prio ? q : qq, a.n_queues);
         }
         const bool done = hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req,
                                                        a.req_out, my, wt, lane, pr, b0, b1, st);
@@ -1683,9 +1738,10 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             for (int i = 0; i < 8; i++) st[i] = own_st[64 * i + lane];
         } else {
             have = false;
+            if (lane == 0u) balance_done();  // no longer behind anyone (kPrioBalance)
         }
     }
-    fused_retire(a.ctl, lane);
+    fused_retire(a.ctl, lane, &waves_retired);
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -1839,25 +1895,29 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
-    if (variant == kVariantCu || variant == 11 || (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
+    if (variant == kVariantCu || variant == 11 || variant == 12 || (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
         // k waves per SIMD, one workgroup of 4k waves per CU
         const uint32_t k = (tiles + 4u * cu_count() - 1u) / (4u * cu_count());
         const uint32_t wg_waves = 4u * std::min(k, kCuMaxWavesPerSimd);
         static bool attr = false;
         if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<false>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
-            if (e != hipSuccess) return e;
+            for (const void* f : {(const void*)sha256_msgs_cu_kernel<false, false>,
+                                  (const void*)sha256_msgs_cu_kernel<true, false>,
+                                  (const void*)sha256_msgs_cu_kernel<false, true>})
+                if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds))
+                    return e;
             attr = true;
         }
         const uint32_t cgrid = (tiles + wg_waves - 1u) / wg_waves;
         if (variant == 11)
-            sha256_msgs_cu_kernel<true><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            sha256_msgs_cu_kernel<true, false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order,
+                                                                                     n, out);
+        else if (variant == 12)
+            sha256_msgs_cu_kernel<false, true><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order,
+                                                                                     n, out);
         else
-            sha256_msgs_cu_kernel<false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            sha256_msgs_cu_kernel<false, false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order,
+                                                                                      n, out);
         return hipGetLastError();
     }
     if (variant == kVariantDirect)

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Config-3 launch forms, same box (GPU): the fused plan's overlapped launch
 with chains (steady state) and without (a stream's first cycle: tiles only),
-and the CU-block request kernel alone.  Kernel time by HIP events."""
+and the CU-block request kernel alone.  Kernel time by HIP events.
+Usage: exp_overlap.py [reps] [overlap tile priority modes: balance progress queue ...]
+(MIRSHA_FUSED_OVERLAP_PRIO, read with MIRSHA_AB=1 on every launch)."""
 import json
 import os
 import sys
@@ -17,6 +19,7 @@ from mirbft_amd.engine import KERNEL_FUSED, KERNEL_MSGS  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    modes = sys.argv[2:] or [None]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     s = torch.cuda.Stream(dev)
@@ -50,12 +53,18 @@ def main():
         return round(ms / max(k, 1) * 1e3, 1)
 
     for _ in range(2):
-        out.setdefault("overlap_chains_us", []).append(timed(
-            lambda: eng.pipeline_overlap_device(plan, *args, d_req[0].data_ptr(), d_req[1].data_ptr(),
-                                                d_bat.data_ptr()), KERNEL_FUSED))
-        out.setdefault("overlap_tiles_only_us", []).append(timed(
-            lambda: eng.pipeline_overlap_device(plan, *args, d_req[0].data_ptr(), 0, d_bat.data_ptr()),
-            KERNEL_FUSED))
+        for m in modes:
+            sfx = f"_{m}" if m else ""
+            if m:
+                os.environ["MIRSHA_AB"] = "1"
+                os.environ["MIRSHA_FUSED_OVERLAP_PRIO"] = m
+            out.setdefault("overlap_chains_us" + sfx, []).append(timed(
+                lambda: eng.pipeline_overlap_device(plan, *args, d_req[0].data_ptr(), d_req[1].data_ptr(),
+                                                    d_bat.data_ptr()), KERNEL_FUSED))
+            out.setdefault("overlap_tiles_only_us" + sfx, []).append(timed(
+                lambda: eng.pipeline_overlap_device(plan, *args, d_req[0].data_ptr(), 0, d_bat.data_ptr()),
+                KERNEL_FUSED))
+            os.environ.pop("MIRSHA_FUSED_OVERLAP_PRIO", None)
         out.setdefault("fused_us", []).append(timed(
             lambda: eng.hash_requests_then_batches_device(plan, *args, d_req[0].data_ptr(), d_bat.data_ptr()),
             KERNEL_FUSED))
