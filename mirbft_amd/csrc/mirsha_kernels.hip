@@ -1618,11 +1618,11 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // runs the segment when its own first tile reaches block seg_at.
     constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
     uint32_t seg = kNoSeg, seg_at = 0u;
-    if (a.n_split && !list_block && slot == last) {
+    if (a.n_split && !list_block && slot == (a.split_host_first ? 0u : last)) {
         const uint32_t h = (blockIdx.x - a.list_waves) * 4u + simd;
         if (h < a.n_split * a.seg_per_tile) {
             seg = h;
-            seg_at = (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
+            seg_at = a.split_host_first ? 0xFFFFFFFFu : (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
         }
     }
     // The first tile of a wave in its own queue is static: queue q holds one

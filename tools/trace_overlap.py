@@ -73,6 +73,8 @@ def main():
                "simd_tiles": {int(k): int(v) for k, v in zip(*np.unique(simd_tiles, return_counts=True))},
                "simd_end_by_tiles": {int(k): pcts(simd_end[simd_tiles == k]) for k in np.unique(simd_tiles)},
                "slot_end_us": {int(k): pcts(us(te[slot == k])) for k in np.unique(slot)},
+               "simd_end_by_xcc": {int(x): pcts(simd_end[(keys >> 20) == x]) for x in np.unique(keys >> 20)},
+               "tile_start_by_xcc": {int(x): pcts(us(ts[xcc == x])) for x in np.unique(xcc)},
                "active_waves_10us": active,
                "group_end_us": pcts(us(gend[gend > 0])) if form == "chains" and (gend > 0).any() else None}
         print(json.dumps(res), flush=True)
