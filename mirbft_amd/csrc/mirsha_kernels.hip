@@ -1619,7 +1619,10 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
     uint32_t seg = kNoSeg, seg_at = 0u;
     if (a.n_split && !list_block && slot == (a.split_host_first ? 0u : last)) {
-        const uint32_t h = (blockIdx.x - a.list_waves) * 4u + simd;
+        // (first-queue hosts from the grid's end: the last queue's tiles are
+        // dealt from its start, so SIMDs left without one host first)
+        const uint32_t hs = (blockIdx.x - a.list_waves) * 4u + simd;
+        const uint32_t h = a.split_host_first ? a.tile_blocks * 4u - 1u - hs : hs;
         if (h < a.n_split * a.seg_per_tile) {
             seg = h;
             seg_at = a.split_host_first ? 0xFFFFFFFFu : (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;

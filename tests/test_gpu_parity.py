@@ -665,17 +665,26 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
     plan.close()
 
 
-@pytest.mark.parametrize("pace,n_tiles", [(1, 1100), (2, 2200), (4, 4200)])
-def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles):
+@pytest.mark.parametrize("pace,n_tiles,knobs", [
+    (1, 1100, {}), (2, 2200, {}), (4, 4200, {}),
+    (4, 4200, {"MIRSHA_FUSED_SPLIT_HOST": "last"}),   # segments interleaved in the last queue's tiles
+    (4, 4200, {"MIRSHA_FUSED_EXTRA_SPLIT": "300"}),   # last-queue tiles split beyond the overflow
+    (2, 2200, {"MIRSHA_FUSED_EXTRA_SPLIT": "250"}),
+])
+def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles, knobs):
     """More request tiles than the fused launch has tile-wave slots: the
-    overflow tiles run as block-range segments hosted one per SIMD (midstate
-    through memory, sequential flags).  Mixed lengths (split tiles of
-    different block counts than their hosts'), shared / null list entries;
-    three runs on one plan (monotone segment flags), then overlapped cycles
-    and the flush; bit-exact vs the oracle."""
+    overflow tiles run as block-range segments (midstate through memory,
+    sequential flags) hosted by the first queue's waves after their own tile
+    (fused runs; or interleaved in the last queue's tiles, overlapped runs and
+    the A/B form), optionally with more of the last queue split.  Mixed
+    lengths (split tiles of different block counts than their hosts'), shared
+    / null list entries; three runs on one plan (monotone segment flags), then
+    overlapped cycles and the flush; bit-exact vs the oracle."""
     torch = _torch()
     monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_FUSED_PACE", str(pace))
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
     arena, off, lens, idx, first = _irregular(60 + pace, 64 * n_tiles - 17, 2048, 60, 1300, 300)
     plan = engine.pipeline(lens.size, idx, first, lens, mode="fused")
     n_split, per_tile = plan.split_tiles()
