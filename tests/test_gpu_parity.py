@@ -668,7 +668,7 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
 @pytest.mark.parametrize("pace,n_tiles,knobs", [
     (1, 1100, {}), (2, 2200, {}), (4, 4200, {}),
     (4, 4200, {"MIRSHA_FUSED_SPLIT_HOST": "last"}),   # segments interleaved in the last queue's tiles
-    (4, 4200, {"MIRSHA_FUSED_EXTRA_SPLIT": "300"}),   # last-queue tiles split beyond the overflow
+    (4, 4200, {"MIRSHA_FUSED_EXTRA_SPLIT": "60"}),    # last-queue tiles split beyond the overflow
     (2, 2200, {"MIRSHA_FUSED_EXTRA_SPLIT": "250"}),
 ])
 def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles, knobs):
