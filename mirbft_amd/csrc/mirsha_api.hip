@@ -1276,11 +1276,13 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.split_first = p->split_first;
     a.seg_per_tile = p->seg_per_tile;
     a.seg_nominal_nb = p->seg_nominal_nb;
-    // Segment hosts (FusedArgs::split_host_first): fused runs -> the first
-    // queue's waves after their own tile; overlapped runs -> interleaved in the
-    // last queue's (their waves end together).  A/B: MIRSHA_FUSED_SPLIT_HOST=first|last.
-    a.split_host_first = (!overlap && p->pace >= 2) ? 1u : 0u;
-    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_SPLIT_HOST")) a.split_host_first = strcmp(e, "first") == 0;
+    // Segment hosts (FusedArgs::split_host): interleaved in the last queue's
+    // tiles.  A/B: MIRSHA_FUSED_SPLIT_HOST=q hosts on queue q's waves after
+    // their own tile (fused runs only; overlapped runs keep the interleave:
+    // their waves end together).
+    a.split_host = p->pace - 1u;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_SPLIT_HOST"))
+        if (!overlap) a.split_host = std::min<uint32_t>((uint32_t)atoi(e), p->pace - 1u);
     a.seg_epoch = p->seg_runs;
     // Overlapped cycles: no chain waits on these tiles, so no queue order to
     // keep: the SIMD's tile waves at priorities by progress rank (kPrioBalance).

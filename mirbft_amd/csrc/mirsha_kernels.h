@@ -155,12 +155,12 @@ struct FusedArgs {
     // done at seg_epoch * seg_per_tile + k + 1).  So no SIMD takes a fifth
     // tile: the overflow spreads as one short segment per SIMD.
     uint32_t n_split, split_first, seg_per_tile, seg_nominal_nb;  // split tiles [split_first, + n_split)
-    // Segment hosts: 0 = the last queue's waves, segment k when the host's own
-    // tile reaches block k * seg_nominal_nb / seg_per_tile; 1 = the FIRST
-    // queue's waves, once their own tile is done (fused runs: the last queue
-    // is the launch's critical path, the first queue's waves are idle after
-    // their tile).
-    uint32_t split_host_first;
+    // Segment hosts: the waves of queue split_host.  The last queue's waves
+    // run segment k when their own tile reaches block k * seg_nominal_nb /
+    // seg_per_tile (interleaved); an earlier queue's waves once their own
+    // tile is done (fused runs: the last queue is the launch's critical path,
+    // the earlier queues' waves are idle after their tile).
+    uint32_t split_host;
     // Overlapped cycles: tile waves at the request kernel's progress
     // priorities instead of their queue's (nothing waits on this run's tiles).
     uint32_t tile_prio_progress;

@@ -1618,14 +1618,15 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // runs the segment when its own first tile reaches block seg_at.
     constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
     uint32_t seg = kNoSeg, seg_at = 0u;
-    if (a.n_split && !list_block && slot == (a.split_host_first ? 0u : last)) {
-        // (first-queue hosts from the grid's end: the last queue's tiles are
+    if (a.n_split && !list_block && slot == min(a.split_host, last)) {
+        // (after-tile hosts from the grid's end: the last queue's tiles are
         // dealt from its start, so SIMDs left without one host first)
+        const bool after = a.split_host < last;
         const uint32_t hs = (blockIdx.x - a.list_waves) * 4u + simd;
-        const uint32_t h = a.split_host_first ? a.tile_blocks * 4u - 1u - hs : hs;
+        const uint32_t h = after ? a.tile_blocks * 4u - 1u - hs : hs;
         if (h < a.n_split * a.seg_per_tile) {
             seg = h;
-            seg_at = a.split_host_first ? 0xFFFFFFFFu : (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
+            seg_at = after ? 0xFFFFFFFFu : (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
         }
     }
     // The first tile of a wave in its own queue is static: queue q holds one

@@ -667,16 +667,17 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
 
 @pytest.mark.parametrize("pace,n_tiles,knobs", [
     (1, 1100, {}), (2, 2200, {}), (4, 4200, {}),
-    (4, 4200, {"MIRSHA_FUSED_SPLIT_HOST": "last"}),   # segments interleaved in the last queue's tiles
-    (4, 4200, {"MIRSHA_FUSED_EXTRA_SPLIT": "60"}),    # last-queue tiles split beyond the overflow
-    (2, 2200, {"MIRSHA_FUSED_EXTRA_SPLIT": "250"}),
+    (4, 4200, {"MIRSHA_FUSED_SPLIT_HOST": "0"}),      # segments on the first queue's waves after their tile
+    (4, 4200, {"MIRSHA_FUSED_SPLIT_HOST": "1"}),
+    (4, 4200, {"MIRSHA_FUSED_EXTRA_SPLIT": "60", "MIRSHA_FUSED_SPLIT_HOST": "1"}),  # more of the last queue split
+    (2, 2200, {"MIRSHA_FUSED_EXTRA_SPLIT": "250", "MIRSHA_FUSED_SPLIT_HOST": "0"}),
 ])
 def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles, knobs):
     """More request tiles than the fused launch has tile-wave slots: the
     overflow tiles run as block-range segments (midstate through memory,
-    sequential flags) hosted by the first queue's waves after their own tile
-    (fused runs; or interleaved in the last queue's tiles, overlapped runs and
-    the A/B form), optionally with more of the last queue split.  Mixed
+    sequential flags) interleaved in the last queue's tiles, or (fused runs,
+    A/B) on an earlier queue's waves after their own tile, optionally with
+    more of the last queue split.  Mixed
     lengths (split tiles of different block counts than their hosts'), shared
     / null list entries; three runs on one plan (monotone segment flags), then
     overlapped cycles and the flush; bit-exact vs the oracle."""
