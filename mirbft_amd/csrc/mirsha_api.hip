@@ -1117,15 +1117,8 @@ int fused_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_
     p->n_split = p->seg_per_tile = p->seg_nominal_nb = 0;
     p->seg_nb.clear();
     const uint32_t hosts = 4u * tile_blocks;
-    // A/B (MIRSHA_FUSED_EXTRA_SPLIT=x): x more of the last queue's tiles split
-    // (their waves idle), so the last queue -- the chains' final stretch --
-    // holds fewer positions.
-    uint32_t extra_split = 0;
-    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_EXTRA_SPLIT"))
-        if (P >= 2) extra_split = std::min<uint32_t>((uint32_t)atoi(e), p->n_tiles - p->q_first[P - 1]);
-    if (len && p->n_tiles + extra_split > p->tile_waves) {
-        const uint32_t ns = std::min(p->n_tiles - p->q_first[P >= 2 ? P - 1 : 0],
-                                     p->n_tiles > p->tile_waves ? p->n_tiles - p->tile_waves + extra_split : extra_split);
+    if (len && p->n_tiles > p->tile_waves) {
+        const uint32_t ns = p->n_tiles - p->tile_waves;
         auto tile_blocks_of = [&](uint32_t t) {
             uint32_t m = 0;
             for (uint32_t i = 64u * t; i < std::min(n_req, 64u * t + 64u); i++)
@@ -1276,13 +1269,6 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     a.split_first = p->split_first;
     a.seg_per_tile = p->seg_per_tile;
     a.seg_nominal_nb = p->seg_nominal_nb;
-    // Segment hosts (FusedArgs::split_host): interleaved in the last queue's
-    // tiles.  A/B: MIRSHA_FUSED_SPLIT_HOST=q hosts on queue q's waves after
-    // their own tile (fused runs only; overlapped runs keep the interleave:
-    // their waves end together).
-    a.split_host = p->pace - 1u;
-    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_SPLIT_HOST"))
-        if (!overlap) a.split_host = std::min<uint32_t>((uint32_t)atoi(e), p->pace - 1u);
     a.seg_epoch = p->seg_runs;
     // Overlapped cycles: no chain waits on these tiles, so no queue order to
     // keep: the SIMD's tile waves at priorities by progress rank (kPrioBalance).

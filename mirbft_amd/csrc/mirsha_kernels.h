@@ -24,7 +24,7 @@ enum : int {
 };
 inline bool variant_valid(int v) {
     return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair ||
-           v == kVariantCu || v == 11 || v == 12;
+           v == kVariantCu || v == 11;
 }
 constexpr uint32_t kCuMaxWavesPerSimd = 4;
 uint32_t cu_count();
@@ -155,14 +155,9 @@ struct FusedArgs {
     // done at seg_epoch * seg_per_tile + k + 1).  So no SIMD takes a fifth
     // tile: the overflow spreads as one short segment per SIMD.
     uint32_t n_split, split_first, seg_per_tile, seg_nominal_nb;  // split tiles [split_first, + n_split)
-    // Segment hosts: the waves of queue split_host.  The last queue's waves
-    // run segment k when their own tile reaches block k * seg_nominal_nb /
-    // seg_per_tile (interleaved); an earlier queue's waves once their own
-    // tile is done (fused runs: the last queue is the launch's critical path,
-    // the earlier queues' waves are idle after their tile).
-    uint32_t split_host;
-    // Overlapped cycles: tile waves at the request kernel's progress
-    // priorities instead of their queue's (nothing waits on this run's tiles).
+    // Tile priorities: 0 = their queue's (fused runs); 1 = the request
+    // kernel's progress priorities; 2 = by progress rank among the SIMD's tile
+    // waves (overlapped cycles: nothing waits on this run's tiles).
     uint32_t tile_prio_progress;
     unsigned long long seg_epoch;
     const uint32_t* seg_nb;            // blocks of each split tile

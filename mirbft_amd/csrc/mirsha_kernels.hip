@@ -236,13 +236,16 @@ __device__ __forceinline__ void fixed_prio(uint32_t p) {
 
 // hash_tile<kFused>'s fprio: priority by rank of progress among the tile waves
 // of the SIMD (FusedArgs::tile_prio_progress == 2, overlapped cycles).  Each
-// wave publishes its block in its LDS word (bal[slot]; an idle or finished
+// wave publishes its block in its LDS word (g_bal_prog; an idle or finished
 // wave's word is kBalDone) and, before each block, takes priority 3 minus the
 // number of the SIMD's waves it is ahead of: the wave furthest behind wins
 // issue.  With one fixed priority after a few blocks the arbiter's age order
 // ran the SIMD's waves one after another instead (config 3's overlapped
 // launch: waves ending at ~420 / 450 / 600 / 760 us, the last ~150 us at one
-// wave per SIMD, tools/trace_overlap.py); by rank they end together.
+// wave per SIMD, tools/trace_overlap.py); by rank they end together
+// (profiles/r03q, r03r: 706 -> 662 us).  The CU-block request kernel is
+// better off without it (677 vs 646 us, profiles/r03w): there no segment
+// host falls behind.
 constexpr uint32_t kPrioBalance = 5;
 constexpr uint32_t kBalDone = 0xFFFFFFFFu;
 // [SIMD][hardware wave slot] (HW_ID's SIMD_ID and WAVE_ID fields: read with
@@ -279,7 +282,7 @@ __device__ __forceinline__ void balance_done() {
 // rounds: with 4 waves per SIMD started together (config 3) the waves reach
 // their staging at the same time and the one-at-a-time form left the SIMD
 // short of issuable waves there (643 us per config-3 launch, profiles/r03b).
-template <bool kNoYield, bool kBalance = false>
+template <bool kNoYield>
 __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc, const uint32_t vo[4],
                                                     const uint32_t sel[4], uint32_t L, uint32_t min_l, bool uni,
                                                     bool tail_ok, const TailWords& tw, uint32_t wave_nb,
@@ -342,7 +345,7 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
         pad_uniform(blk, w);
         const bool next = blk + 1u < wave_nb;  // wave-uniform
         uint32_t wn[16];
-        if constexpr (kBalance) balance_prio(blk); else progress_prio(blk);
+        progress_prio(blk);
         compress_asm_hooked<kNoYield>(st, w, blk < nb, [&](int k) {
             if (k == 0 && next) {
                 write_tile(blk + 1u);
@@ -357,7 +360,7 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
     if (tail_ok) {  // final block (<= 16 message bytes), staged during the loop's last block
         const uint32_t blk = wave_nb - 1u;
         pad_block_uniform<4>(w, 64u * blk, min_l, false);
-        if constexpr (kBalance) balance_prio(blk); else progress_prio(blk);
+        progress_prio(blk);
         if (blk < nb) compress_asm_tail(st, w, tw);
     }
 }
@@ -371,7 +374,7 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
 // [b0, b1) of the tile, from the midstate in st (H0 when b0 == 0).  Returns
 // true when the range reached the tile's end: the digest is then stored;
 // otherwise st holds the midstate after block b1 - 1.
-template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false, bool kBalance = false>
+template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false>
 __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
@@ -539,8 +542,8 @@ __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uin
         const uint32_t loop_nb = tail_ok ? wave_nb - 1u : wave_nb;
         if constexpr (kPf) {
             if (far && aligned && b0 == 0u && finished) {
-                hash_tile_pipelined<kNoYield, kBalance>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb,
-                                                        lane, my, st);
+                hash_tile_pipelined<kNoYield>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb, lane, my,
+                                              st);
                 goto digest;
             }
         }
@@ -689,7 +692,7 @@ __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_ms
 // its SIMDs in cyclic order: exactly k waves per SIMD.  At k <= 4 a wave may
 // hold 128 VGPRs, so the next block's chunks are prefetched into registers.
 constexpr uint32_t kCuLds = 96u * 1024u;
-template <bool kNoYield, bool kBalance>
+template <bool kNoYield>
 __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* __restrict__ arena,
                                                                  uint64_t arena_len,
                                                                  const uint64_t* __restrict__ off,
@@ -700,13 +703,9 @@ __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * (blockDim.x >> 6) + wv;
-    if constexpr (kBalance) {
-        if (threadIdx.x < 64u) g_bal_prog[threadIdx.x] = kBalDone;
-        __syncthreads();
-    }
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<true, false, false, true, kNoYield, kBalance>(arena, arena_len, off, len, order, n, out,
-                                                            cu_lds + 256u * wv, t, lane);
+    hash_tile<true, false, false, true, kNoYield>(arena, arena_len, off, len, order, n, out, cu_lds + 256u * wv, t,
+                                                  lane);
 }
 
 // ---- overlapped cycles: this cycle's request tiles + the previous cycle's
@@ -1618,15 +1617,11 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // runs the segment when its own first tile reaches block seg_at.
     constexpr uint32_t kNoSeg = 0xFFFFFFFFu;
     uint32_t seg = kNoSeg, seg_at = 0u;
-    if (a.n_split && !list_block && slot == min(a.split_host, last)) {
-        // (after-tile hosts from the grid's end: the last queue's tiles are
-        // dealt from its start, so SIMDs left without one host first)
-        const bool after = a.split_host < last;
-        const uint32_t hs = (blockIdx.x - a.list_waves) * 4u + simd;
-        const uint32_t h = after ? a.tile_blocks * 4u - 1u - hs : hs;
+    if (a.n_split && !list_block && slot == last) {
+        const uint32_t h = (blockIdx.x - a.list_waves) * 4u + simd;
         if (h < a.n_split * a.seg_per_tile) {
             seg = h;
-            seg_at = after ? 0xFFFFFFFFu : (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
+            seg_at = (h % a.seg_per_tile) * a.seg_nominal_nb / a.seg_per_tile;
         }
     }
     // The first tile of a wave in its own queue is static: queue q holds one
@@ -1714,7 +1709,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             b0 = ob0;
             b1 = seg != kNoSeg ? seg_at : 0xFFFFFFFFu;
             // (overlapped cycles: no chain waits on these tiles, so no queue
-            // order to keep -- the request kernel's progress priorities)
+            // order to keep -- priorities by progress rank, kPrioBalance)
             pr = a.tile_prio_progress == 2u ? kPrioBalance
                  : a.tile_prio_progress     ? kPrioProgress
                                             : prio_of(a.steal_own_prio ? q : qq, a.n_queues);
@@ -1899,29 +1894,25 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
-    if (variant == kVariantCu || variant == 11 || variant == 12 || (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
+    if (variant == kVariantCu || variant == 11 || (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
         // k waves per SIMD, one workgroup of 4k waves per CU
         const uint32_t k = (tiles + 4u * cu_count() - 1u) / (4u * cu_count());
         const uint32_t wg_waves = 4u * std::min(k, kCuMaxWavesPerSimd);
         static bool attr = false;
         if (!attr) {
-            for (const void* f : {(const void*)sha256_msgs_cu_kernel<false, false>,
-                                  (const void*)sha256_msgs_cu_kernel<true, false>,
-                                  (const void*)sha256_msgs_cu_kernel<false, true>})
-                if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds))
-                    return e;
+            hipError_t e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<false>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<true>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
+            if (e != hipSuccess) return e;
             attr = true;
         }
         const uint32_t cgrid = (tiles + wg_waves - 1u) / wg_waves;
         if (variant == 11)
-            sha256_msgs_cu_kernel<true, false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order,
-                                                                                     n, out);
-        else if (variant == 12)
-            sha256_msgs_cu_kernel<false, true><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order,
-                                                                                     n, out);
+            sha256_msgs_cu_kernel<true><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         else
-            sha256_msgs_cu_kernel<false, false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order,
-                                                                                      n, out);
+            sha256_msgs_cu_kernel<false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantDirect)

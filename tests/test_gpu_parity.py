@@ -665,27 +665,17 @@ def test_fused_list_tiles_config3(engine, monkeypatch, list_tiles):
     plan.close()
 
 
-@pytest.mark.parametrize("pace,n_tiles,knobs", [
-    (1, 1100, {}), (2, 2200, {}), (4, 4200, {}),
-    (4, 4200, {"MIRSHA_FUSED_SPLIT_HOST": "0"}),      # segments on the first queue's waves after their tile
-    (4, 4200, {"MIRSHA_FUSED_SPLIT_HOST": "1"}),
-    (4, 4200, {"MIRSHA_FUSED_EXTRA_SPLIT": "60", "MIRSHA_FUSED_SPLIT_HOST": "1"}),  # more of the last queue split
-    (2, 2200, {"MIRSHA_FUSED_EXTRA_SPLIT": "250", "MIRSHA_FUSED_SPLIT_HOST": "0"}),
-])
-def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles, knobs):
+@pytest.mark.parametrize("pace,n_tiles", [(1, 1100), (2, 2200), (4, 4200)])
+def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles):
     """More request tiles than the fused launch has tile-wave slots: the
     overflow tiles run as block-range segments (midstate through memory,
-    sequential flags) interleaved in the last queue's tiles, or (fused runs,
-    A/B) on an earlier queue's waves after their own tile, optionally with
-    more of the last queue split.  Mixed
+    sequential flags) interleaved in the last queue's tiles.  Mixed
     lengths (split tiles of different block counts than their hosts'), shared
     / null list entries; three runs on one plan (monotone segment flags), then
     overlapped cycles and the flush; bit-exact vs the oracle."""
     torch = _torch()
     monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_FUSED_PACE", str(pace))
-    for k, v in knobs.items():
-        monkeypatch.setenv(k, v)
     arena, off, lens, idx, first = _irregular(60 + pace, 64 * n_tiles - 17, 2048, 60, 1300, 300)
     plan = engine.pipeline(lens.size, idx, first, lens, mode="fused")
     n_split, per_tile = plan.split_tiles()
