@@ -548,7 +548,66 @@ __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uin
             }
         }
         const uint32_t loop_end = min(loop_nb, b1);
-        for (uint32_t blk = b0; blk < loop_end; blk++) {
+        // Fused launch, aligned in-range tiles: the block loop below with the
+        // loads as LDS-DMA (buffer_load_dwordx4 ... lds), block b+1's issued as
+        // soon as block b's words are read back, so they land while b's rounds
+        // run.  The fused launch runs 4 waves per SIMD and fewer as its queues
+        // end (the last queue runs its final stretch alone), where the
+        // register-staged loader's load latency was exposed every block; the
+        // register prefetch of hash_tile_pipelined does not fit its 128 VGPRs.
+        // Lane l of piece j fetches slot 64 j + l of the swizzled tile
+        // (lds_slot's inverse), so the transposed read back is the loader's.
+        bool dma = false;
+        if constexpr (kFused) dma = far && aligned;
+        if (dma) {
+            const uint32_t qd = (lane & 3u) ^ ((lane >> 4) & 3u);
+            uint32_t vd[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                vd[j] = (uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) + 16u * qd;
+            auto issue_dma = [&](uint32_t blk) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                        rsrc, (__attribute__((address_space(3))) void*)(my + 64 * j), 16, vd[j], 64u * blk, 0, 0);
+            };
+            // (bounds through readfirstlane: the block index is the DMA's
+            // scalar offset, and a bound the compiler takes for divergent
+            // turned every DMA into a waterfall loop)
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
+            const uint32_t d1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)loop_end);
+            const uint32_t dmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)min_l);
+            if (d0 < d1) issue_dma(d0);
+            for (uint32_t blk = d0; blk < d1; blk++) {
+                const uint32_t soff = 64u * blk;
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block blk landed in LDS
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+                    w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
+                }
+                // the reads are back before the next DMA overwrites the tile
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (blk + 1u < d1) issue_dma(blk + 1u);
+#pragma unroll
+                for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(w[k]);
+                if (soff + 64u > dmin) {  // wave-uniform
+                    uint32_t wnb;  // (opaque copy, as below)
+                    asm volatile("s_mov_b32 %0, %1" : "=s"(wnb) : "s"(wave_nb));
+                    if (uni) {
+                        pad_block_uniform(w, soff, dmin, wnb - blk == 1u);
+                    } else {  // each lane pads its own message
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            pad_words(soff + 16u * (uint32_t)k, L, blk + 1u == nb, (uint32_t)k, &w[4 * k]);
+                    }
+                }
+                block_prio(blk);
+                if (blk < nb) compress_asm(st, w);
+            }
+        }
+        for (uint32_t blk = dma ? loop_end : b0; blk < loop_end; blk++) {
             const uint32_t soff = 64u * blk;
             uint32_t w[16];
             stage(blk, w, lane, false);
