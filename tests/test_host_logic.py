@@ -74,3 +74,24 @@ def test_arena_windows_cover_and_bound():
         assert sorted(o.tolist()) == list(range(i1 - i0))
         blk = sharding.blocks_for_len(ln[i0:i1][o]).astype(np.int64)
         assert np.all(np.diff(blk) <= 0)
+
+
+def test_fused_lds_dma_mapping_matches_the_tile_swizzle():
+    """The fused launch's LDS-DMA loader (mirsha_kernels.hip, hash_tile): lane l
+    of DMA piece j lands in 16-byte slot 64 j + l of the wave's tile and must
+    fetch the chunk the transposed read expects there -- message 16 j + l / 4,
+    quarter (l & 3) ^ ((l >> 4) & 3) -- i.e. the inverse of lds_slot(m, q) =
+    4 m + (q ^ ((m >> 2) & 3)).  Every (message, quarter) exactly once."""
+    def lds_slot(m, q):
+        return 4 * m + (q ^ ((m >> 2) & 3))
+
+    seen = set()
+    for j in range(4):
+        for lane in range(64):
+            m = 16 * j + (lane >> 2)
+            q = (lane & 3) ^ ((lane >> 4) & 3)
+            assert lds_slot(m, q) == 64 * j + lane
+            # the kernel derives the offset from the register loader's (quarter lane & 3)
+            assert 16 * q == 16 * (lane & 3) + 16 * (((lane & 3) ^ ((lane >> 4) & 3)) - (lane & 3))
+            seen.add((m, q))
+    assert seen == {(m, q) for m in range(64) for q in range(4)}
