@@ -75,7 +75,7 @@ def parse():
     p.add_argument("--config", type=int, default=2, choices=[1] + sorted(CONFIGS),
                    help="BASELINE config (1 = small-cycle latency of the host API)")
     p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
-    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6, 10, 11],
+    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6, 10, 11, 12],
                    help="0 = LDS-staged loader (latency forms for small launches), 1 = direct per-lane loads, "
                         "4 = low-occupancy kernel, 5 = LDS kernel only, 6 = pair kernel")
     p.add_argument("--windows", action="store_true",
@@ -93,6 +93,9 @@ def parse():
                    help="PMC traffic per launch, keyed by kernel_source_key(); written by profiles/profile.sh")
     p.add_argument("--no-overlap-extra", dest="overlap_extra", action="store_false",
                    help="skip the overlapped-cycles figure (configs 2/3 with a sequential plan)")
+    p.add_argument("--no-config3-leg", dest="config3_leg", action="store_false",
+                   help="config 2 runs: skip the config-3 leg (fused step, overlapped cycles, sequential request "
+                        "kernel) measured after the headline")
     p.add_argument("--pipeline", default="auto", choices=["auto", "none", "fused", "sequential", "overlap"],
                    help="auto: mirsha_pipeline plan, AUTO mode (fused launch for long chains, else request "
                         "kernel then list kernel); none: plain device API (request kernel, then batch kernel); "
@@ -346,11 +349,16 @@ class BatchWorkload:
         return out
 
     def cpu_baseline(self, seconds):
-        """Oracle (C port of processor.go:133-143 with SHA-NI compression, the
-        instruction class Go's crypto/sha256 uses on amd64) on the host cores:
-        the serial Processor on one core (the headline), and the order-
-        preserving ProcessorWorkPool analogue with HashWorkers = NumCPU() (the
-        reference default, processor.go:406-408) and with the cgroup quota."""
+        """Oracle (C port of processor.go:133-143) on the host cores: the
+        serial Processor on one core with SHA-NI compression (the headline), the
+        same with the portable scalar FIPS 180-4 compression (`go114_class`:
+        the reference pins Go 1.13/1.14, .travis.yml:5-6 and go.mod:3, whose
+        amd64 crypto/sha256 has no SHA-NI path -- Go added one in 1.21 -- but
+        an AVX2/BMI2 block function), and the order-preserving
+        ProcessorWorkPool analogue with HashWorkers = NumCPU() (the reference
+        default, processor.go:406-408) and with the cgroup quota.  SHA-NI is
+        the headline because it is the FASTER CPU figure: the conservative
+        baseline for the GPU."""
         o = _oracle()
         stride, bs = self.stride, self.bs
         n = min(self.n, 1 << 16)
@@ -368,6 +376,18 @@ class BatchWorkload:
         per = n + first.size - 1
         done1, dt1 = res[1]
         facts = _cpu_facts()
+        # Scalar FIPS compression on the same sample, one core (Go 1.14 class).
+        o.force_impl(0)
+        try:
+            ds, dts = _time_cpu(one, seconds / 4, (1,))[1]
+        finally:
+            o.force_impl(-1)
+        go114 = {"value": ds * per / dts, "unit": "digests/s", "cores": 1,
+                 "sample": f"{ds} passes of the headline sample, {dts:.1f} s",
+                 "note": "portable scalar FIPS 180-4 compression (gcc -O2), no SHA-NI: the instruction class of "
+                         "the reference's Go 1.13/1.14 crypto/sha256 on amd64 (.travis.yml:5-6, go.mod:3), whose "
+                         "AVX2/BMI2 block function vectorises the message schedule and has no SHA-NI path "
+                         "(Go added SHA-NI in 1.21)"}
         # Pool legs on a larger sample (whole config up to 2^20 requests), so
         # per-pass thread start-up is noise; batch digests single-threaded, as
         # the state machine consumes them (processResults, state_machine.go:377-433).
@@ -395,7 +415,9 @@ class BatchWorkload:
             "value": done1 * per / dt1, "unit": "digests/s", "cores": 1, "kind": "port",
             "sample": f"{done1} passes x ({n} requests x {stride} B + {first.size - 1} BatchSize-{bs} batch "
                       f"digests), {dt1:.1f} s, oracle C port of processor.go:133-143 (serial Processor), "
-                      f"SHA-NI compression (stand-in for Go crypto/sha256 amd64 asm)",
+                      f"SHA-NI compression (faster than the reference's Go 1.14 crypto/sha256, which has no "
+                      f"SHA-NI path: a conservative baseline; the Go 1.14-class figure is go114_class)",
+            "go114_class": go114,
             "pool": {**legs,
                      "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361): workers pull "
                              "requests from a shared counter; numcpu = HashWorkers = runtime.NumCPU() = the affinity "
@@ -745,6 +767,69 @@ def small_cycle_bench(a, eng):
     }), flush=True)
 
 
+def config3_leg(a, eng, dev):
+    """BASELINE config 3 (2^18 x 4 KB requests + VerifyBatch-500 digests) as a
+    leg of the default run, after config 2's timed region and self-check
+    (rank 0, N = 1): the fused plan's step (request + VerifyBatch chains in
+    one launch, readiness counters), its dominant-kernel time and roofline
+    fraction, the overlapped-cycles figure on the same plan, the sequential
+    plan's request kernel (the CU-block kernel, 4 waves per SIMD), and a
+    self-check against the oracle on a sample.  Data generated on the device
+    before any timed region; ~3-5 s."""
+    import argparse as _ap
+
+    t_start = time.perf_counter()
+    steps = min(a.steps, 20)
+    out = {}
+    for mode in ("auto", "sequential"):
+        a3 = _ap.Namespace(**vars(a))
+        a3.config, a3.requests, a3.pipeline, a3.steps, a3.warmup = 3, 0, mode, steps, 3
+        wl = BatchWorkload(a3, eng, dev, 0)
+        for _ in range(a3.warmup):
+            wl.step()
+        torch.cuda.synchronize(dev)
+        t_pw = time.perf_counter()
+        while (time.perf_counter() - t_pw) < 0.15:  # untimed pre-warm at this load
+            wl.step()
+            torch.cuda.synchronize(dev)
+        eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED] if mode == "auto" else range(32))
+        eng.set_timing(True)
+        eng.reset_timing()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            wl.step()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        eng.set_timing(False)
+        wl.after()
+        kname, n_k, ms_k, work_blocks, hbm = wl.dominant()
+        kms = ms_k / max(n_k, 1)
+        tops = work_blocks * OPS_PER_COMPRESSION / (ms_k / steps * 1e-3) / 1e12
+        tkey = kernel_source_key(a.variant)
+        traffic, _ = lookup_traffic(a.traffic_file, tkey, 3, kname)
+        leg = {"plan": wl.plan.mode_name, "ms_per_step": dt / steps * 1e3,
+               "digests_per_s": wl.digests * steps / dt, "kernel": kname, "avg_launch_ms": kms,
+               "frac": tops / VALU_PEAK_TOPS, "compressions": work_blocks, "traffic": traffic,
+               "traffic_key": tkey, "self_check": wl.self_check()}
+        if wl.plan.mode_name == "fused":
+            leg["overlap_cycles"] = wl.overlap_cycles()
+            leg["frac_note"] = "request + VerifyBatch compressions over the fused launch's time"
+        else:
+            leg["frac_note"] = "request compressions over the request kernel's time (the batch chains follow)"
+            leg["batch_kernel_ms"] = wl.batch_ms() / steps
+        eng.set_timing_mask(range(32))
+        out[wl.plan.mode_name] = leg
+        if wl.plan is not None:
+            wl.plan.close()
+        del wl
+        torch.cuda.empty_cache()
+    out["workload"] = f"config3: {CONFIGS[3][3]}"
+    out["steps"] = steps
+    out["leg_seconds"] = time.perf_counter() - t_start
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -884,6 +969,12 @@ def main():
                     "note": "clock probe: 8 waves/SIMD of register-only compressions (the request kernel's "
                             "round form), right after the timed region"}
 
+    # Config 3 (the north_star's 4 KB target) as a leg of the default run.
+    c3 = None
+    if rank == 0 and world == 1 and a.config == 2 and a.config3_leg and a.requests == 0:
+        eng.set_stream(stream.cuda_stream)
+        c3 = config3_leg(a, eng, dev)
+
     cpu = wl.cpu_baseline(a.cpu_seconds) if rank == 0 and world == 1 and a.cpu_seconds > 0 else None
 
     # Per-rank evidence (control plane, after the timed region): which device
@@ -918,7 +1009,7 @@ def main():
                 "workload": f"config{a.config}: {wl.desc}",
                 **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair", 10: "cu", 11: "cu_noyield"}[a.variant],
+                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair", 10: "cu", 11: "cu_noyield", 12: "cu_dma"}[a.variant],
             },
             "gb_per_s_hashed": gbps,
             "roofline": {
@@ -956,6 +1047,7 @@ def main():
                                                      "barriers and max / sum reductions of timings only"},
             "pcie_inclusive": pcie,
             "cgo_path": cgo,
+            "config3": c3,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -284,6 +284,12 @@ int mirsha_pipeline_create_mode(mirsha_ctx* ctx, uint32_t n_req, const uint32_t*
                                 const uint32_t* list_first, uint32_t n_lists, int mode, mirsha_pipeline** out);
 void mirsha_pipeline_destroy(mirsha_pipeline* p);
 int mirsha_pipeline_mode(const mirsha_pipeline* p);
+/* 1 if a FUSED (or AUTO -> fused) plan was built SEQUENTIAL instead because
+ * the placement probe at creation found the device not dealing a
+ * workgroup's waves evenly over the SIMDs (the fused launch deals its static
+ * roles by SIMD; its kernel stays correct under any placement, but stacked
+ * waves would run slower than the sequential plan); 0 otherwise. */
+int mirsha_pipeline_fallback(const mirsha_pipeline* p);
 /* Synchronises the context stream and reports a fused run whose readiness
  * watchdog expired (MIRSHA_EHIP; never expected, the launch is deadlock-free
  * by construction).  MIRSHA_OK otherwise.
@@ -372,6 +378,52 @@ int mirsha_hash_batch_multi(const int* devices, int ndev, const uint8_t* arena,
 /* Contexts mirsha_hash_batch_multi keeps per device between calls: freed here
  * (optional; otherwise at process exit). */
 void mirsha_multi_release(void);
+
+/* The multi-GPU drop-in: a Go caller's Ready() cycle crosses PCIe at about
+ * one link's rate per call (config 2: ~50 GB/s), so one device caps every
+ * host-memory caller; the reference's pool scales with cores instead
+ * (processor.go:401-410, HashWorkers = runtime.NumCPU()).  A mirsha_multi
+ * holds one context per listed device (its own stream, pinned staging ring,
+ * PCIe link) and one host worker per device with its own packing pool (an
+ * equal share of the host threads).  Each call validates the slice lists,
+ * cuts the requests into contiguous ranges of equal bytes (one per device;
+ * ranges may be empty), and runs mirsha_hash_slices / mirsha_submit_slices
+ * on every range in parallel; digests land at digests_out[32*i] in origin
+ * order.  A device may be listed twice (two contexts on it: tests).  With
+ * MIRSHA_SUBMIT_DEDUP each device deduplicates within its own range.
+ * Single-caller, like a context.  At most 16 devices. */
+typedef struct mirsha_multi mirsha_multi;
+int mirsha_multi_create(const int* devices, int ndev, mirsha_multi** out);
+void mirsha_multi_destroy(mirsha_multi* m);
+const char* mirsha_multi_last_error(const mirsha_multi* m);
+int mirsha_multi_devices(const mirsha_multi* m);
+/* Context of device index k (0 <= k < ndev) for per-device settings and
+ * diagnostics (mirsha_ctx_set_variant, timing); owned by m. */
+mirsha_ctx* mirsha_multi_ctx(mirsha_multi* m, int k);
+/* Request-range cut of the last call: first_out[k] = first request of device
+ * index k, first_out[ndev] = n.  Returns ndev + 1 (entries written: min(cap, ndev + 1)). */
+int mirsha_multi_last_cut(const mirsha_multi* m, uint32_t* first_out, int cap);
+int mirsha_hash_slices_multi(mirsha_multi* m, const uint8_t* const* slice_ptr,
+                             const uint64_t* slice_len, const uint32_t* slice_first, uint32_t n,
+                             uint8_t* digests_out);
+/* The same over a caller arena (mirsha_hash_batch on every range): with a
+ * page-locked arena from mirsha_multi_host_alloc every device DMAs its range
+ * straight from it over its own link (the Go binding's GPUHasherMulti packs
+ * one Ready() cycle into that arena with GOMAXPROCS goroutines). */
+int mirsha_hash_arena_multi(mirsha_multi* m, const uint8_t* arena, uint64_t arena_len,
+                            const uint64_t* off, const uint32_t* len, uint32_t n, uint8_t* digests_out);
+/* Page-locked host memory usable by every device of m (portable); free with mirsha_host_free. */
+int mirsha_multi_host_alloc(mirsha_multi* m, uint64_t bytes, void** out);
+/* Asynchronous form (mirsha_submit_slices on every range): up to 4
+ * submissions in flight; wait / poll cover every device's range of every
+ * submission up to `ticket`.  The caller may reuse the slices when submit returns. */
+int mirsha_submit_slices_multi(mirsha_multi* m, const uint8_t* const* slice_ptr,
+                               const uint64_t* slice_len, const uint32_t* slice_first, uint32_t n,
+                               uint8_t* digests_out, int flags, uint64_t* ticket_out);
+int mirsha_wait_multi(mirsha_multi* m, uint64_t ticket);
+int mirsha_poll_multi(mirsha_multi* m, uint64_t ticket, int* done);
+/* mirsha_ctx_host_profile of device index k's last call (its range only). */
+int mirsha_multi_host_profile(const mirsha_multi* m, int k, double* ms_out, int n);
 
 /* ------------------------------------------- benchmark / test utility only */
 /* Device-side synthetic request stream, byte-identical to the

@@ -7,7 +7,8 @@ hand-written gfx950 HIP kernels behind the C-ABI in include/mirsha.h.
 """
 from . import eventlog, hashdata, sharding
 from ._lib import MirshaError, MirshaUnavailable
-from .engine import CheckpointChains, Engine, SliceArrays, Ticket, bucket_order, dedup_plan, device_count, hash_batch_multi
+from .engine import (CheckpointChains, Engine, MultiEngine, SliceArrays, Ticket, bucket_order, dedup_plan, device_count,
+                     hash_batch_multi)
 from .processor import (ActionResults, Actions, GpuHash, HashRequest, HashResult, PendingResults, Processor,
                         ProcessorWorkPool, gpu_hasher)
 
@@ -23,6 +24,7 @@ __all__ = [
     "bucket_order",
     "device_count",
     "hash_batch_multi",
+    "MultiEngine",
     "eventlog",
     "hashdata",
     "sharding",

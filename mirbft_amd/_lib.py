@@ -79,6 +79,7 @@ SIGNATURES = {
     ),
     "mirsha_pipeline_destroy": (None, [c_void_p]),
     "mirsha_pipeline_mode": (c_int, [c_void_p]),
+    "mirsha_pipeline_fallback": (c_int, [c_void_p]),
     "mirsha_pipeline_status": (c_int, [c_void_p, c_void_p]),
     "mirsha_pipeline_trace": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "mirsha_pipeline_shape": (c_int, [c_void_p, _u32p, _u32p, _u32p]),
@@ -102,6 +103,22 @@ SIGNATURES = {
         [c_void_p, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p],
     ),
     "mirsha_multi_release": (None, []),
+    "mirsha_multi_create": (c_int, [c_void_p, c_int, POINTER(c_void_p)]),
+    "mirsha_multi_destroy": (None, [c_void_p]),
+    "mirsha_multi_last_error": (c_char_p, [c_void_p]),
+    "mirsha_multi_devices": (c_int, [c_void_p]),
+    "mirsha_multi_ctx": (c_void_p, [c_void_p, c_int]),
+    "mirsha_multi_last_cut": (c_int, [c_void_p, _u32p, c_int]),
+    "mirsha_hash_slices_multi": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p]),
+    "mirsha_submit_slices_multi": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_int, _u64p],
+    ),
+    "mirsha_hash_arena_multi": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p]),
+    "mirsha_multi_host_alloc": (c_int, [c_void_p, c_uint64, POINTER(c_void_p)]),
+    "mirsha_wait_multi": (c_int, [c_void_p, c_uint64]),
+    "mirsha_poll_multi": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
+    "mirsha_multi_host_profile": (c_int, [c_void_p, c_int, POINTER(c_double), c_int]),
     "mirsha_synth_requests_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_uint32, c_void_p]),
     "mirsha_synth_mixed_lengths_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p]),
     "mirsha_synth_mixed_device": (c_int, [c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_void_p]),

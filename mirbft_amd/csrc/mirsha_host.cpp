@@ -115,6 +115,7 @@ namespace {
 // is created on first use and never destroyed (workers park on a condition
 // variable until the process exits).
 thread_local bool t_in_pool_job = false;
+thread_local int t_pool_slot = 0, t_pool_threads = 0;  // use_pool
 
 class Pool {
   public:
@@ -176,22 +177,33 @@ class Pool {
     uint64_t gen_ = 0;
 };
 
+Pool& pool() {
+    static Pool* p = new Pool(max_threads() - 1);
+    if (t_pool_slot <= 0) return *p;
+    static std::mutex mu;
+    static Pool* extra[kMaxPools] = {};
+    std::lock_guard<std::mutex> g(mu);
+    Pool*& q = extra[t_pool_slot];
+    if (!q) q = new Pool(std::max(t_pool_threads, 1) - 1);
+    return *q;
+}
+
+}  // namespace
+
 int max_threads() {
     int t = env_threads();
     if (t <= 0) t = std::min(std::max((int)std::thread::hardware_concurrency(), 1), 16);
     return t;
 }
 
-Pool& pool() {
-    static Pool* p = new Pool(max_threads() - 1);
-    return *p;
+void use_pool(int slot, int threads) {
+    t_pool_slot = (slot > 0 && slot < kMaxPools) ? slot : 0;
+    t_pool_threads = t_pool_slot ? std::max(threads, 1) : 0;
 }
-
-}  // namespace
 
 int threads_for(uint64_t bytes, uint32_t n) {
     if (n < 2 || bytes < (4ull << 20)) return 1;
-    int t = max_threads();
+    int t = t_pool_slot ? t_pool_threads : max_threads();
     const uint64_t by_bytes = bytes / (1ull << 20);  // >= 1 MiB per thread
     t = (int)std::min<uint64_t>((uint64_t)t, std::max<uint64_t>(1, by_bytes));
     return std::min<int>(t, (int)n);

@@ -25,6 +25,19 @@ int threads_for(uint64_t bytes, uint32_t n);
 // fn(lo, hi) over contiguous index ranges covering [0, n), on `threads` threads.
 void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, uint32_t)>& fn);
 
+// Host threads of the process: min(hardware threads, 16), or MIRSHA_HOST_THREADS.
+int max_threads();
+
+// Pool of the calling thread's parallel_for: slot 0 = the process pool
+// (max_threads() workers, the default); slots 1..kMaxPools-1 = pools of
+// `threads` threads (workers + the caller), created on first use and kept,
+// for callers that pack for several devices at once (mirsha_multi: one per
+// device, each with its share of the host threads, so the devices' packing
+// runs side by side instead of queueing for one pool).  threads_for() is
+// capped at the selected pool's size.
+constexpr int kMaxPools = 17;
+void use_pool(int slot, int threads);
+
 // 64-bit fingerprint of concat(ptr[s] for s in [s0, s1)): depends only on the
 // concatenated bytes, not on how they are sliced.  NOT cryptographic: equal
 // fingerprints are always confirmed byte for byte before two requests share

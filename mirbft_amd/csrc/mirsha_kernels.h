@@ -21,10 +21,15 @@ enum : int {
     kVariantLdsOnly = 5,
     kVariantPair = 6,
     kVariantCu = 10,      // CU-block form (one workgroup per CU, prefetching; at most 4 tiles per SIMD)
+    // A/B forms of the CU-block kernel, accepted only with MIRSHA_AB=1:
+    kVariantCuNoYield = 11,  // no-yield rounds
+    kVariantCuDma = 12,      // LDS-DMA block loads one block ahead (the fused launch's loader)
 };
+const char* ab_getenv(const char* name);
 inline bool variant_valid(int v) {
+    if (v == kVariantCuNoYield || v == kVariantCuDma) return ab_getenv("MIRSHA_AB") != nullptr;
     return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair ||
-           v == kVariantCu || v == 11;
+           v == kVariantCu;
 }
 constexpr uint32_t kCuMaxWavesPerSimd = 4;
 uint32_t cu_count();
@@ -159,6 +164,9 @@ struct FusedArgs {
     // kernel's progress priorities; 2 = by progress rank among the SIMD's tile
     // waves (overlapped cycles: nothing waits on this run's tiles).
     uint32_t tile_prio_progress;
+    // Test only (MIRSHA_AB=1 MIRSHA_TEST_PLACEMENT=remap): every wave reads
+    // SIMD 0, so the in-kernel identity remap of a non-cyclic placement runs.
+    uint32_t test_placement;
     unsigned long long seg_epoch;
     const uint32_t* seg_nb;            // blocks of each split tile
     uint32_t* seg_state;
@@ -172,6 +180,9 @@ constexpr uint32_t kPacedRingOff = 64u * 1024u;
 constexpr uint32_t kPacedLds = 97u * 1024u;
 constexpr uint32_t kPacedMaxPace = 4;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
+// Placement probe of the fused launch's block shape: *broken |= 1 when some
+// block's 4P waves are not dealt P per SIMD (test != 0: report broken).
+hipError_t launch_placement_probe(uint32_t grid, uint32_t pace, uint32_t* broken, uint32_t test, hipStream_t s);
 // Streaming checkpoint chains (state: midstate h[8], pending digest words
 // pend[8], digest count cnt per chain), see mirsha_kernels.hip.
 hipError_t launch_chains_absorb(const uint8_t* digests, const uint32_t* pos, const uint32_t* act, const uint32_t* afirst,

@@ -17,6 +17,7 @@
 // XOR-swizzled so both the ds_write_b128 (8-lane groups, 128 contiguous bytes)
 // and the per-lane ds_read_b128 (16-lane groups) are bank-conflict free.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "mirsha_kernels.h"
@@ -372,10 +373,15 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
 // (hash_tile_pipelined).
 // Block range (the fused launch's split tiles, LDS loader only): blocks
 // [b0, b1) of the tile, from the midstate in st (H0 when b0 == 0).  Returns
-// true when the range reached the tile's end: the digest is then stored;
-// otherwise st holds the midstate after block b1 - 1.
-template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false>
-__device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
+// kTileDone when the range reached the tile's end (the digest is then
+// stored), kTilePaused when it did not (st_io then holds the midstate after
+// block b1 - 1), and kTileSkipped when the range starts at or past the tile's
+// end (b0 > 0): the tile's run-time messages are shorter than the ones its
+// plan cut the ranges for, an earlier range already stored the digest, and
+// this one does nothing (no digest, no midstate).
+constexpr uint32_t kTilePaused = 0, kTileDone = 1, kTileSkipped = 2;
+template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false, bool kDma = false>
+__device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
                                           uint4* my, uint32_t t, uint32_t lane, uint32_t fprio = 0,
@@ -414,6 +420,7 @@ __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uin
     // wave-uniform block count (SGPR: scalar block-loop tests).
     const uint32_t max_l = wave_max(valid ? L : 0u);
     const uint32_t wave_nb = blocks_for_len(max_l);
+    if (b0 != 0u && b0 >= wave_nb) return kTileSkipped;  // wave-uniform (run lengths < plan lengths)
 
     // Bytes past arena_len inside the last dword are never part of a message
     // (they are masked by the padding logic), so the range rounds up to 4.
@@ -540,7 +547,7 @@ __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uin
         // branch inside it: two round copies joined inside the loop made the
         // register allocator spill (64 VGPRs is the 8-wave budget).
         const uint32_t loop_nb = tail_ok ? wave_nb - 1u : wave_nb;
-        if constexpr (kPf) {
+        if constexpr (kPf && !kDma) {
             if (far && aligned && b0 == 0u && finished) {
                 hash_tile_pipelined<kNoYield>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb, lane, my,
                                               st);
@@ -558,7 +565,7 @@ __device__ __forceinline__ bool hash_tile(const uint8_t* __restrict__ arena, uin
         // Lane l of piece j fetches slot 64 j + l of the swizzled tile
         // (lds_slot's inverse), so the transposed read back is the loader's.
         bool dma = false;
-        if constexpr (kFused) dma = far && aligned;
+        if constexpr (kFused || kDma) dma = far && aligned;
         if (dma) {
             const uint32_t qd = (lane & 3u) ^ ((lane >> 4) & 3u);
             uint32_t vd[4];
@@ -700,7 +707,7 @@ digest:
     if (!finished) {  // a split tile's range: hand the midstate back
 #pragma unroll
         for (int i = 0; i < 8; i++) st_io[i] = st[i];
-        return false;
+        return kTilePaused;
     }
     if (valid) {
         if constexpr (kFused) {
@@ -718,7 +725,7 @@ digest:
             store_digest(out, msg, st);
         }
     }
-    return true;
+    return kTileDone;
 }
 
 // One wave per workgroup: a workgroup's slot and LDS are released only when
@@ -751,7 +758,10 @@ __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_ms
 // its SIMDs in cyclic order: exactly k waves per SIMD.  At k <= 4 a wave may
 // hold 128 VGPRs, so the next block's chunks are prefetched into registers.
 constexpr uint32_t kCuLds = 96u * 1024u;
-template <bool kNoYield>
+// kMode: 0 = register-prefetching block loop (hash_tile_pipelined, the
+// product form), 1 = the same with no-yield rounds, 2 = the fused launch's
+// one-block-ahead LDS-DMA block loop (A/B forms, variants 11 and 12).
+template <int kMode>
 __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* __restrict__ arena,
                                                                  uint64_t arena_len,
                                                                  const uint64_t* __restrict__ off,
@@ -763,8 +773,8 @@ __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* 
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * (blockDim.x >> 6) + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<true, false, false, true, kNoYield>(arena, arena_len, off, len, order, n, out, cu_lds + 256u * wv, t,
-                                                  lane);
+    hash_tile<true, false, false, true, kMode == 1, kMode == 2>(arena, arena_len, off, len, order, n, out,
+                                                                cu_lds + 256u * wv, t, lane);
 }
 
 // ---- overlapped cycles: this cycle's request tiles + the previous cycle's
@@ -1622,34 +1632,55 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     const uint32_t wv = threadIdx.x >> 6;
     const __amdgpu_buffer_rsrc_t drs =
         __builtin_amdgcn_make_buffer_rsrc((void*)a.list_digests, (short)0, (int)(32u * a.n_req), 0x00020000);
-    // Slot = this wave's rank among the block's waves on its SIMD (HW_ID).  A
-    // workgroup's waves are dealt to the CU's SIMDs in cyclic order
-    // (MI355X_MICROARCH.md, LDS section), so a block of 4P waves puts exactly
-    // P on every SIMD: one tile wave per queue per SIMD (the static first
-    // tiles below), slot-0 waves on SIMDs 0 and 1 for a list block's pair.  A
-    // wave that finds itself at slot >= P proves that placement broken for its
-    // block (some SIMD then lacks a slot, so a static tile or the pair would
-    // be missing): it sets the plan's error word, and the run fails closed
-    // (block-batched claims that tolerate any placement measured 12 us slower
-    // per config-3 launch, profiles/r03l).
+    // Identity = (simd, slot): the wave's SIMD (HW_ID) and its rank among the
+    // block's waves on that SIMD.  A workgroup's waves are dealt to the CU's
+    // SIMDs in cyclic order (MI355X_MICROARCH.md, LDS section), so a block of
+    // 4P waves puts exactly P on every SIMD: one tile wave per queue per SIMD
+    // (the static first tiles below), slot-0 waves on SIMDs 0 and 1 for a list
+    // block's pair, the last slot hosting split-tile segments.  Every role
+    // derives from the identity, so any other placement is remapped, not
+    // failed: after the count, the waves at slot >= P (extras) take the
+    // identities no wave holds (SIMDs with fewer than P waves), in order, and
+    // every (simd, slot) of the block is held by exactly one wave -- some then
+    // share a physical SIMD, which is slower but complete.  (Round 3 failed
+    // such a run closed; plans probe the placement at creation and fall back
+    // to the sequential plan when it is not cyclic, mirsha_api.hip.)
+    // FusedArgs::test_placement (MIRSHA_AB=1 MIRSHA_TEST_PLACEMENT=remap)
+    // makes every wave read SIMD 0, so the remap runs on real hardware.
     __shared__ uint32_t simd_waves[4];
+    __shared__ uint32_t extra_ticket;
     __shared__ uint32_t waves_retired;
     static_assert(kPacedRingOff + sizeof(FusedPairRing) <= kPacedLds && kPacedRingOff >= 4096u * kPacedMaxPace * 4u,
                   "paced LDS: staging tiles, then the pair ring");
     FusedPairRing& ring = *reinterpret_cast<FusedPairRing*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedRingOff);
     const bool list_block = blockIdx.x < a.list_waves;  // list_waves carries the number of LIST BLOCKS
     if (threadIdx.x < 4u) simd_waves[threadIdx.x] = 0u;
-    if (threadIdx.x == 0u) waves_retired = 0u;
+    if (threadIdx.x == 0u) waves_retired = extra_ticket = 0u;
     if (threadIdx.x < 64u) g_bal_prog[threadIdx.x] = kBalDone;  // tile progress (kPrioBalance)
     if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = ring.aborted = 0u;
     __syncthreads();
     uint32_t hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    const uint32_t simd = (hw >> 4) & 3u;
+    const uint32_t P = blockDim.x >> 8;
+    uint32_t simd = a.test_placement ? 0u : (hw >> 4) & 3u;
     uint32_t slot = 0u;
     if (lane == 0u) slot = atomicAdd(&simd_waves[simd], 1u);
     slot = (uint32_t)__shfl((int)slot, 0, 64);
-    if (slot >= (blockDim.x >> 8) && lane == 0u) raise_error(a.err);
+    __syncthreads();  // every wave counted
+    if (slot >= P) {  // wave-uniform: an extra wave takes the next identity no wave holds
+        uint32_t e = 0u;
+        if (lane == 0u) e = atomicAdd(&extra_ticket, 1u);
+        e = (uint32_t)__shfl((int)e, 0, 64);
+        for (uint32_t s4 = 0; s4 < 4u; s4++) {
+            const uint32_t have = min(simd_waves[s4], P), miss = P - have;
+            if (e < miss) {
+                simd = s4;
+                slot = have + e;
+                break;
+            }
+            e -= miss;
+        }
+    }
     bool own = true, tiles = true;
     if (list_block && (slot != 0u || simd > 1u)) {  // not the pair: a tile wave, or idle
         tiles = !(a.list_tiles == 0u || (a.list_tiles == 1u && simd <= 1u));
@@ -1773,13 +1804,17 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
                  : a.tile_prio_progress     ? kPrioProgress
                                             : prio_of(a.steal_own_prio ? q : qq, a.n_queues);
         }
-        const bool done = hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req,
-                                                       a.req_out, my, wt, lane, pr, b0, b1, st);
-        if (!done && !is_seg) {  // own tile paused at seg_at
+        // (a segment's range is cut from the plan's lengths; with shorter
+        // messages at run time an earlier segment may already have finished
+        // the tile: this one is then kTileSkipped and only raises its flag)
+        const uint32_t rs = hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req,
+                                                         a.req_out, my, wt, lane, pr, b0, b1, st);
+        const bool done = rs == kTileDone;
+        if (rs == kTilePaused && !is_seg) {  // own tile paused at seg_at
             ob0 = seg_at;
             continue;
         }
-        if (!done) store_midstate_sc1(a.seg_state, s_i, lane, st);
+        if (rs == kTilePaused) store_midstate_sc1(a.seg_state, s_i, lane, st);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (done) {
             if (!is_seg && a.trace && lane == 0) a.trace[3 * t + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1800,6 +1835,25 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
         }
     }
     fused_retire(a.ctl, lane, &waves_retired);
+}
+
+// Placement probe (fused plan creation): blocks of the fused launch's shape
+// (4P waves, kPacedLds of LDS: one block per CU) count their waves per SIMD;
+// a block whose count is not P on every SIMD sets *broken.  With test != 0
+// every wave reads SIMD 0 (tests: the plan's sequential fallback).
+__global__ __launch_bounds__(kPacedMaxThreads) void placement_probe_kernel(uint32_t* broken, uint32_t test) {
+    __shared__ uint32_t cnt[4];
+    if (threadIdx.x < 4u) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const uint32_t simd = test ? 0u : (hw >> 4) & 3u;
+    if ((threadIdx.x & 63u) == 0u) atomicAdd(&cnt[simd], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0u) {
+        const uint32_t P = blockDim.x >> 8;
+        if (cnt[0] != P || cnt[1] != P || cnt[2] != P || cnt[3] != P) atomicOr(broken, 1u);
+    }
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -1921,17 +1975,33 @@ uint32_t pair_max_groups() {
     return v;
 }
 
-// Compute units of the current device (cached per device).
+// Compute units of the current device (cached per device; relaxed atomics:
+// mirsha_hash_batch_multi launches from one thread per device).
 uint32_t cu_count() {
-    static uint32_t cached[64] = {};
+    static std::atomic<uint32_t> cached[64] = {};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256u;
-    if (!cached[dev]) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-        cached[dev] = (uint32_t)v;
+    uint32_t v = cached[dev].load(std::memory_order_relaxed);
+    if (!v) {
+        int a = 0;
+        if (hipDeviceGetAttribute(&a, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || a <= 0) a = 256;
+        v = (uint32_t)a;
+        cached[dev].store(v, std::memory_order_relaxed);
     }
-    return cached[dev];
+    return v;
+}
+
+// The dynamic-LDS limit of kernel `fn` (one of 5 forms) raised on the
+// current device, once per (device, form): per-device flags, set with atomics
+// (mirsha_hash_batch_multi launches from one thread per device).
+hipError_t dyn_lds_attr(const void* fn, int form, uint32_t bytes) {
+    static std::atomic<uint8_t> done[64][5] = {};
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    if (dev >= 0 && dev < 64 && done[dev][form].load(std::memory_order_acquire)) return hipSuccess;
+    if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes)) return e;
+    if (dev >= 0 && dev < 64) done[dev][form].store(1, std::memory_order_release);
+    return hipSuccess;
 }
 
 hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
@@ -1953,25 +2023,23 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
-    if (variant == kVariantCu || variant == 11 || (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
+    if (variant == kVariantCu || variant == kVariantCuNoYield || variant == kVariantCuDma ||
+        (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
         // k waves per SIMD, one workgroup of 4k waves per CU
         const uint32_t k = (tiles + 4u * cu_count() - 1u) / (4u * cu_count());
         const uint32_t wg_waves = 4u * std::min(k, kCuMaxWavesPerSimd);
-        static bool attr = false;
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<false>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void*)sha256_msgs_cu_kernel<true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCuLds);
-            if (e != hipSuccess) return e;
-            attr = true;
-        }
+        const int form = variant == kVariantCuNoYield ? 1 : variant == kVariantCuDma ? 2 : 0;
+        const void* fn = form == 1 ? (const void*)sha256_msgs_cu_kernel<1>
+                         : form == 2 ? (const void*)sha256_msgs_cu_kernel<2>
+                                     : (const void*)sha256_msgs_cu_kernel<0>;
+        if (hipError_t e = dyn_lds_attr(fn, form, kCuLds)) return e;
         const uint32_t cgrid = (tiles + wg_waves - 1u) / wg_waves;
-        if (variant == 11)
-            sha256_msgs_cu_kernel<true><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+        if (variant == kVariantCuNoYield)
+            sha256_msgs_cu_kernel<1><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+        else if (variant == kVariantCuDma)
+            sha256_msgs_cu_kernel<2><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         else
-            sha256_msgs_cu_kernel<false><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            sha256_msgs_cu_kernel<0><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantDirect)
@@ -2020,14 +2088,16 @@ hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const u
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s) {
     if (grid == 0) return hipSuccess;
     if (pace < 1 || pace > kPacedMaxPace || a.n_queues != pace) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void*)sha256_fused_paced_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPacedLds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (hipError_t e = dyn_lds_attr((const void*)sha256_fused_paced_kernel, 3, kPacedLds)) return e;
     sha256_fused_paced_kernel<<<grid, 256u * pace, kPacedLds, s>>>(a);
+    return hipGetLastError();
+}
+
+hipError_t launch_placement_probe(uint32_t grid, uint32_t pace, uint32_t* broken, uint32_t test, hipStream_t s) {
+    if (grid == 0) return hipSuccess;
+    if (pace < 1 || pace > kPacedMaxPace) return hipErrorInvalidValue;
+    if (hipError_t e = dyn_lds_attr((const void*)placement_probe_kernel, 4, kPacedLds)) return e;
+    placement_probe_kernel<<<grid, 256u * pace, kPacedLds, s>>>(broken, test);
     return hipGetLastError();
 }
 

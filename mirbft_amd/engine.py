@@ -404,6 +404,8 @@ class Pipeline:
                                                                 _ptr(fs), int(fs.size) - 1, m, ctypes.byref(h)))
         self.handle = h
         self.mode = int(self._lib.mirsha_pipeline_mode(h))
+        # 1: a fused plan built sequential after its placement probe (mirsha_pipeline_fallback)
+        self.fallback = int(self._lib.mirsha_pipeline_fallback(h))
         self.n_req = int(n_req)
         self.n_lists = int(fs.size) - 1
 
@@ -521,8 +523,119 @@ def hash_batch_multi(devices: Iterable[int], arena, off, length) -> np.ndarray:
     return out
 
 
+class MultiEngine:
+    """The multi-GPU drop-in (mirsha_multi, include/mirsha.h): one context
+    per listed device, requests cut into contiguous ranges of equal bytes,
+    each range packed, copied over its device's own PCIe link and hashed in
+    parallel; digests in origin order.  A device may be listed twice (two
+    contexts on one GPU: tests on a one-GPU box)."""
+
+    def __init__(self, devices: Iterable[int]):
+        self._lib = _lib.load()
+        devs = np.ascontiguousarray(list(devices), dtype=np.int32)
+        h = ctypes.c_void_p()
+        check(self._lib.mirsha_multi_create(_ptr(devs), int(devs.size), ctypes.byref(h)))
+        self.handle = h
+        self.devices = [int(d) for d in devs]
+        self._outstanding = {}
+
+    def _check(self, rc: int) -> None:
+        if rc != _lib.MIRSHA_OK:
+            raw = self._lib.mirsha_multi_last_error(self.handle)
+            raise MirshaError(rc, raw.decode() if raw else "")
+
+    def context(self, k: int):
+        """The ctypes handle of device index k's context (owned by this object)."""
+        return self._lib.mirsha_multi_ctx(self.handle, int(k))
+
+    def set_variant(self, variant: int) -> None:
+        for k in range(len(self.devices)):
+            check(self._lib.mirsha_ctx_set_variant(self.context(k), int(variant)))
+
+    def hash_slice_arrays(self, sl: "SliceArrays") -> np.ndarray:
+        out = np.empty((sl.n, 32), dtype=np.uint8)
+        if sl.n:
+            self._check(self._lib.mirsha_hash_slices_multi(self.handle, sl.ptr_p, sl.len_p, sl.first_p, sl.n,
+                                                           _ptr(out)))
+        return out
+
+    def hash_slices(self, requests) -> np.ndarray:
+        sl = requests if isinstance(requests, SliceArrays) else SliceArrays.from_requests(requests)
+        return self.hash_slice_arrays(sl)
+
+    def hash_arena(self, arena, off, length, out=None) -> np.ndarray:
+        """mirsha_hash_arena_multi: requests packed in one arena (offsets, lengths)."""
+        a = _as_u8(arena)
+        o = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(length, dtype=np.uint32)
+        out = _out_rows(out, o.size)
+        if o.size:
+            self._check(self._lib.mirsha_hash_arena_multi(self.handle, _ptr(a), a.size, _ptr(o), _ptr(ln), o.size,
+                                                          _ptr(out)))
+        return out
+
+    def host_empty(self, nbytes: int) -> np.ndarray:
+        """Page-locked host memory usable by every device (mirsha_multi_host_alloc)."""
+        p = ctypes.c_void_p()
+        self._check(self._lib.mirsha_multi_host_alloc(self.handle, int(nbytes), ctypes.byref(p)))
+        buf = (ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value)
+        arr = np.frombuffer(buf, dtype=np.uint8, count=int(nbytes))
+        import weakref
+
+        weakref.finalize(buf, self._lib.mirsha_host_free, p.value)
+        return arr
+
+    def submit_slices(self, requests, dedup: bool = False) -> "Ticket":
+        sl = requests if isinstance(requests, SliceArrays) else SliceArrays.from_requests(requests)
+        out = np.empty((sl.n, 32), dtype=np.uint8)
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.mirsha_submit_slices_multi(self.handle, sl.ptr_p, sl.len_p, sl.first_p, sl.n,
+                                                         _ptr(out), _lib.MIRSHA_SUBMIT_DEDUP if dedup else 0,
+                                                         ctypes.byref(t)))
+        self._outstanding[t.value] = out
+        for k in [k for k in self._outstanding if k <= t.value - ASYNC_SLOTS]:
+            del self._outstanding[k]
+        return Ticket(t.value, out)
+
+    def wait(self, ticket: "Ticket") -> np.ndarray:
+        self._check(self._lib.mirsha_wait_multi(self.handle, ticket.value))
+        for k in [k for k in self._outstanding if k <= ticket.value]:
+            del self._outstanding[k]
+        return ticket.out
+
+    def poll(self, ticket: "Ticket") -> bool:
+        done = ctypes.c_int(0)
+        self._check(self._lib.mirsha_poll_multi(self.handle, ticket.value, ctypes.byref(done)))
+        return bool(done.value)
+
+    def last_cut(self) -> list:
+        """First request of each device index in the last call, then n."""
+        buf = (ctypes.c_uint32 * (len(self.devices) + 1))()
+        n = self._lib.mirsha_multi_last_cut(self.handle, buf, len(buf))
+        return list(buf)[:n]
+
+    def host_profile(self, k: int) -> dict:
+        buf = (ctypes.c_double * len(Engine.HOST_PHASES))()
+        n = self._lib.mirsha_multi_host_profile(self.handle, int(k), buf, len(Engine.HOST_PHASES))
+        if n < 0:
+            self._check(n)
+        return {key: buf[i] for i, key in enumerate(Engine.HOST_PHASES)}
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self._lib.mirsha_multi_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 __all__ = [
     "Engine",
+    "MultiEngine",
     "CheckpointChains",
     "SliceArrays",
     "Ticket",

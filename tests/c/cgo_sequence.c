@@ -12,6 +12,10 @@
  *   one-request mirsha_hash_batch calls (gpuHash.Sum, the hash.Hash of
  *     processor.go:21)
  *   mirsha_host_free, mirsha_ctx_destroy
+ *   GPUHasherMulti (several devices; here device 0 listed twice):
+ *     mirsha_multi_create, mirsha_multi_host_alloc (portable pinned arena),
+ *     mirsha_hash_arena_multi per cycle, mirsha_submit_slices_multi +
+ *     mirsha_wait_multi, mirsha_host_free, mirsha_multi_destroy
  *
  * Requests are the testengine's (testengine/recorder.go:158-174): client c,
  * reqNo r, data = LE64(c) || "-" || LE64(r), hashed as state_machine.go:313-317
@@ -175,6 +179,65 @@ int main(void) {
 
     mirsha_host_free(arena);
     mirsha_ctx_destroy(ctx);
+    ctx = NULL;
+
+    /* GPUHasherMulti: the 800 requests in one portable pinned arena, cut by
+     * bytes over the devices (HashBatch), then as C slice arrays through the
+     * asynchronous form (SubmitBatch / Wait). */
+    {
+        const int devs[2] = {0, ndev > 1 ? 1 : 0};
+        mirsha_multi* m = NULL;
+        int rc = mirsha_multi_create(devs, 2, &m);
+        if (rc != MIRSHA_OK) {
+            fprintf(stderr, "mirsha_multi_create failed: %d\n", rc);
+            return 2;
+        }
+#define MCHECK(call)                                                                      \
+    do {                                                                                  \
+        int rc_ = (call);                                                                 \
+        if (rc_ != MIRSHA_OK) {                                                           \
+            fprintf(stderr, "%s failed: %d: %s\n", #call, rc_, mirsha_multi_last_error(m)); \
+            exit(2);                                                                      \
+        }                                                                                 \
+    } while (0)
+        void* pa = NULL;
+        MCHECK(mirsha_multi_host_alloc(m, 33ull * n_total + 1, &pa));
+        uint8_t* a = (uint8_t*)pa;
+        uint64_t* off = malloc(8ull * n_total);
+        uint32_t* len = malloc(4ull * n_total);
+        uint8_t* dig = malloc(32ull * n_total);
+        uint64_t p = 0;
+        for (uint32_t i = 0; i < n_total; i++) {
+            off[i] = p;
+            len[i] = pack_request(a + p, i / 200, i % 200);
+            p += len[i];
+        }
+        MCHECK(mirsha_hash_arena_multi(m, a, p, off, len, n_total, dig));
+        for (uint32_t i = 0; i < n_total; i++) print_hex("multi", i, dig + 32ull * i);
+        const uint8_t** ptr = malloc(sizeof(uint8_t*) * n_total);
+        uint64_t* slen = malloc(8ull * n_total);
+        uint32_t* first = malloc(4ull * (n_total + 1));
+        for (uint32_t i = 0; i < n_total; i++) {
+            ptr[i] = a + off[i];
+            slen[i] = len[i];
+            first[i] = i;
+        }
+        first[n_total] = n_total;
+        uint64_t t = 0;
+        memset(dig, 0, 32ull * n_total);
+        MCHECK(mirsha_submit_slices_multi(m, ptr, slen, first, n_total, dig, 0, &t));
+        free(ptr);
+        free(slen);
+        free(first);
+        memset(a, 0, p); /* the caller may reuse its bytes at once */
+        MCHECK(mirsha_wait_multi(m, t));
+        for (uint32_t i = 0; i < n_total; i++) print_hex("amulti", i, dig + 32ull * i);
+        free(off);
+        free(len);
+        free(dig);
+        mirsha_host_free(pa);
+        mirsha_multi_destroy(m);
+    }
     printf("sequence ok\n");
     return 0;
 }

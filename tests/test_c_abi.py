@@ -43,7 +43,7 @@ def test_cgo_sequence_on_gpu(tmp_path, layouts):
     assert "fips ok" in lines and lines[-1] == "sequence ok"
     want = {200 * e["client"] + e["req_no"]: e["sha256"] for e in layouts["testengine_requests"]}
     assert len(want) == 800
-    for tag in ("req", "async"):
+    for tag in ("req", "async", "multi", "amulti"):
         got = {int(i): h for t, i, h in (ln.split() for ln in lines if ln.startswith(tag + " "))}
         assert got == want, tag
 

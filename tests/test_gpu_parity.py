@@ -5,6 +5,7 @@ Run on an MI355X:  python -u -m pytest tests -m gpu -x -v --timeout 120 --timeou
 """
 import ctypes
 import hashlib
+import os
 
 import numpy as np
 import pytest
@@ -22,8 +23,14 @@ pytestmark = pytest.mark.gpu
 EMPTY = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 
 
-@pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR, VARIANT_CU],
-                ids=["lds", "direct", "lowocc", "lds_only", "pair", "cu"])
+# A/B kernel forms (accepted by the library only with MIRSHA_AB=1) join the
+# parametrisation when MIRSHA_TEST_AB_VARIANTS lists them, e.g. "12".
+_AB_VARIANTS = [int(v) for v in os.environ.get("MIRSHA_TEST_AB_VARIANTS", "").split(",") if v.strip()]
+
+
+@pytest.fixture(params=[VARIANT_LDS, VARIANT_DIRECT, VARIANT_LOWOCC, VARIANT_LDS_ONLY, VARIANT_PAIR, VARIANT_CU]
+                + _AB_VARIANTS,
+                ids=["lds", "direct", "lowocc", "lds_only", "pair", "cu"] + [f"ab{v}" for v in _AB_VARIANTS])
 def eng(engine, request):
     engine.set_variant(request.param)
     yield engine
@@ -699,6 +706,83 @@ def test_fused_split_tiles(engine, monkeypatch, pace, n_tiles):
     assert np.array_equal(d_req[0].cpu().numpy(), want_req)
     assert np.array_equal(d_req[1].cpu().numpy(), want_req)
     assert np.array_equal(d_lst.cpu().numpy(), want_lst)
+    plan.close()
+
+
+def test_fused_split_tiles_shorter_run_lengths(engine, monkeypatch):
+    """A plan's split-tile segment ranges are cut from the lengths given at
+    plan creation (a bucketing hint); runs may pass other lengths.  Here the
+    run-time messages are prefixes of the planned ones (a third to a half of
+    their blocks), so a middle segment finishes each split tile and the later
+    segments must do nothing: no second digest store, no second readiness
+    increment.  Runs with the short lengths, then the planned
+    lengths, then the short ones again on one plan; bit-exact every time."""
+    monkeypatch.setenv("MIRSHA_AB", "1")
+    monkeypatch.setenv("MIRSHA_FUSED_PACE", "2")
+    arena, off, lens, idx, first = _irregular(77, 64 * 2200 - 5, 1024, 60, 1300, 900)
+    plan = engine.pipeline(lens.size, idx, first, lens, mode="fused")
+    n_split, per_tile = plan.split_tiles()
+    assert n_split > 0 and per_tile >= 2, (n_split, per_tile)
+    short = (lens // 3).astype(np.uint32)
+    for run_lens in (short, lens, short):
+        want_req = oracle_py.hash_requests(arena, off, run_lens, threads=8)
+        want_lst = oracle_py.batch_digests(want_req, idx, first)
+        for req, lst in _plan_run(engine, plan, arena, off, run_lens, first.size - 1, runs=2):
+            assert np.array_equal(req, want_req)
+            assert np.array_equal(lst, want_lst)
+    plan.close()
+
+
+@pytest.mark.parametrize("placement", ["broken", "remap"])
+def test_fused_placement_fallback(engine, monkeypatch, placement):
+    """The fused launch deals its static roles (first tiles, list pair,
+    segment hosts) by (SIMD, slot).  broken: the plan's placement probe is
+    made to report a non-cyclic dealing (test knob), and the fused plan is
+    built sequential instead (mirsha_pipeline_fallback = 1); remap: the plan
+    stays fused but every wave of the launch reads SIMD 0, so the kernel's
+    identity remap hands the missing (SIMD, slot) roles to the extra waves.
+    Both bit-exact at config-3 shape on a reduced count (split tiles
+    included), over two runs and an overlapped cycle."""
+    torch = _torch()
+    monkeypatch.setenv("MIRSHA_AB", "1")
+    monkeypatch.setenv("MIRSHA_TEST_PLACEMENT", placement)
+    n, data_len, bs = 64 * 4100, 4096, 500
+    stride = 16 + data_len
+    seed = synth.SEED_BASE + 80
+    idx, first = sharding.batch_lists(n, bs)
+    plan = engine.pipeline(n, idx, first, np.full(n, stride), mode="fused")
+    monkeypatch.delenv("MIRSHA_TEST_PLACEMENT")
+    if placement == "broken":
+        assert plan.mode_name == "sequential" and plan.fallback == 1
+    else:
+        assert plan.mode_name == "fused" and plan.fallback == 0
+        assert plan.split_tiles()[0] > 0
+    d_arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    d_off = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+    d_len = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+    d_req = [torch.empty((n, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_bat = torch.empty((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    engine.synth_requests_device(seed, 0, n, data_len, d_arena.data_ptr())
+    arena = oracle_py.gen_requests(seed, 0, n, data_len)
+    want_req = oracle_py.hash_requests(arena, np.arange(n, dtype=np.uint64) * stride, np.full(n, stride), threads=8)
+    want_bat = oracle_py.batch_digests(want_req, idx, first)
+    args = (d_arena.data_ptr(), d_arena.numel(), d_off.data_ptr(), d_len.data_ptr())
+    for _ in range(2):
+        d_req[0].zero_()
+        d_bat.zero_()
+        torch.cuda.synchronize()
+        engine.hash_requests_then_batches_device(plan, *args, d_req[0].data_ptr(), d_bat.data_ptr())
+        plan.status()
+        assert np.array_equal(d_req[0].cpu().numpy(), want_req)
+        assert np.array_equal(d_bat.cpu().numpy(), want_bat)
+    d_bat.zero_()
+    d_req[1].zero_()
+    torch.cuda.synchronize()
+    engine.pipeline_overlap_device(plan, *args, d_req[1].data_ptr(), d_req[0].data_ptr(), d_bat.data_ptr())
+    engine.sync()
+    plan.status()
+    assert np.array_equal(d_req[1].cpu().numpy(), want_req)
+    assert np.array_equal(d_bat.cpu().numpy(), want_bat)
     plan.close()
 
 
