@@ -75,7 +75,7 @@ def parse():
     p.add_argument("--config", type=int, default=2, choices=[1] + sorted(CONFIGS),
                    help="BASELINE config (1 = small-cycle latency of the host API)")
     p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
-    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6, 10, 11, 12],
+    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6, 10, 11, 12, 13, 14, 15],
                    help="0 = LDS-staged loader (latency forms for small launches), 1 = direct per-lane loads, "
                         "4 = low-occupancy kernel, 5 = LDS kernel only, 6 = pair kernel")
     p.add_argument("--windows", action="store_true",
@@ -1009,7 +1009,7 @@ def main():
                 "workload": f"config{a.config}: {wl.desc}",
                 **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair", 10: "cu", 11: "cu_noyield", 12: "cu_dma"}[a.variant],
+                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair", 10: "cu", 11: "cu_noyield", 12: "cu_prefetch", 13: "cu_dma_pipe", 14: "cu_diag_noloads", 15: "cu_diag_noprio"}[a.variant],
             },
             "gb_per_s_hashed": gbps,
             "roofline": {

@@ -77,14 +77,19 @@ void* mirsha_ctx_stream(mirsha_ctx* ctx);
  *     kernel -- schedule and rounds of each compression on two waves on two
  *     SIMDs -- and one of at most 1024 groups (one wave per SIMD) the
  *     low-occupancy kernel: prefetching direct loads, no-yield rounds;
- *     MIRSHA_PAIR=0 in the environment disables the pair forms),
+ *     MIRSHA_AB=1 MIRSHA_PAIR=0 in the environment disables the pair forms,
+ *     an A/B knob read only with MIRSHA_AB=1),
  *     A launch of 1,025..4,096 groups (at most 4 per SIMD) takes the CU-block
  *     kernel: one workgroup of 4k waves per CU, exactly k waves per SIMD,
- *     next-block chunks prefetched into registers.
+ *     each wave's next block DMA'd into its LDS tile during this block.
  * 1 = direct per-lane loads, 4 = the low-occupancy kernel at any size,
  * 5 = the LDS kernel at any size, 6 = the pair kernel at any size,
  * 10 = the CU-block kernel at any size (groups beyond 4 per SIMD run in
  *     later workgroups, one CU at a time).
+ * A/B forms of the CU-block kernel, accepted only with MIRSHA_AB=1 in the
+ * environment (else EINVAL): 11 = register-prefetching block loop with
+ * no-yield rounds, 12 = register-prefetching block loop (round 3's form),
+ * 13 = LDS-DMA with the next block read back mid-block.
  * All are bit-exact.  2, 3, 7, 8 (round-1 A/B forms) are retired: EINVAL. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 

@@ -2495,9 +2495,11 @@ int multi_cut(mirsha_multi* m, const uint8_t* const* slice_ptr, const uint64_t* 
     m->cut.assign(nd + 1, n);
     m->cut[0] = 0;
     for (int k = 1; k < nd; k++) {
-        const uint64_t want = (total * (uint64_t)k + nd - 1) / nd;
-        m->cut[k] = (uint32_t)(std::lower_bound(sum.begin(), sum.end(), want) - sum.begin());
-        m->cut[k] = std::max(m->cut[k], m->cut[k - 1]);
+        // the request boundary nearest to k/nd of the bytes
+        const uint64_t want = (total * (uint64_t)k + nd / 2) / nd;
+        uint32_t i = (uint32_t)(std::lower_bound(sum.begin(), sum.end(), want) - sum.begin());  // sum[i] >= want
+        if (i < n && (i == 0 ? want : want - sum[i - 1]) * 2 > (sum[i] - (i ? sum[i - 1] : 0))) i++;
+        m->cut[k] = std::max(std::min(i, n), m->cut[k - 1]);
     }
     return MIRSHA_OK;
 }

@@ -20,14 +20,18 @@ enum : int {
     kVariantLowOcc = 4,
     kVariantLdsOnly = 5,
     kVariantPair = 6,
-    kVariantCu = 10,      // CU-block form (one workgroup per CU, prefetching; at most 4 tiles per SIMD)
+    kVariantCu = 10,      // CU-block form (one workgroup per CU, LDS-DMA loads one block ahead; <= 4 tiles per SIMD)
     // A/B forms of the CU-block kernel, accepted only with MIRSHA_AB=1:
-    kVariantCuNoYield = 11,  // no-yield rounds
-    kVariantCuDma = 12,      // LDS-DMA block loads one block ahead (the fused launch's loader)
+    kVariantCuNoYield = 11,  // register-prefetching block loop, no-yield rounds
+    kVariantCuPrefetch = 12, // register-prefetching block loop (round 3's product form)
+    kVariantCuDmaPipe = 13,  // LDS-DMA, the next block's words read back mid-block
+    // diagnostics (MIRSHA_AB=1; 14's digests are not valid): the product form
+    kVariantCuDiagNoLoads = 14,  // without its block loads
+    kVariantCuDiagNoPrio = 15,   // without its per-block issue priorities
 };
 const char* ab_getenv(const char* name);
 inline bool variant_valid(int v) {
-    if (v == kVariantCuNoYield || v == kVariantCuDma) return ab_getenv("MIRSHA_AB") != nullptr;
+    if (v >= kVariantCuNoYield && v <= kVariantCuDiagNoPrio) return ab_getenv("MIRSHA_AB") != nullptr;
     return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair ||
            v == kVariantCu;
 }

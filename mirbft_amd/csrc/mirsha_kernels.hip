@@ -375,19 +375,23 @@ __device__ __forceinline__ void hash_tile_pipelined(__amdgpu_buffer_rsrc_t rsrc,
 // [b0, b1) of the tile, from the midstate in st (H0 when b0 == 0).  Returns
 // kTileDone when the range reached the tile's end (the digest is then
 // stored), kTilePaused when it did not (st_io then holds the midstate after
-// block b1 - 1), and kTileSkipped when the range starts at or past the tile's
-// end (b0 > 0): the tile's run-time messages are shorter than the ones its
-// plan cut the ranges for, an earlier range already stored the digest, and
-// this one does nothing (no digest, no midstate).
-constexpr uint32_t kTilePaused = 0, kTileDone = 1, kTileSkipped = 2;
-template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false, bool kDma = false>
+// block b1 - 1).  (A range that starts at or past the tile's end is never
+// passed: the fused launch skips such split-tile segments itself.)
+constexpr uint32_t kTilePaused = 0, kTileDone = 1;
+// kDiag (diagnostic builds of the CU-block kernel only, variants 14 / 15,
+// MIRSHA_AB=1; digests are NOT valid under 1): 1 = no block loads (the
+// rounds run on the LDS tile's stale words), 2 = no per-block s_setprio.
+template <bool kLds, bool kWide, bool kFused = false, bool kPf = false, bool kNoYield = false, bool kDma = false,
+          bool kDmaPipe = false, int kDiag = 0>
 __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena, uint64_t arena_len,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
                                           uint4* my, uint32_t t, uint32_t lane, uint32_t fprio = 0,
                                           uint32_t b0 = 0u, uint32_t b1 = 0xFFFFFFFFu, uint32_t* st_io = nullptr) {
     auto block_prio = [&](uint32_t blk) {
-        if constexpr (kFused) {
+        if constexpr (kDiag == 2) {
+            return;
+        } else if constexpr (kFused) {
             if (fprio == kPrioBalance)
                 balance_prio(blk);
             else if (fprio == kPrioProgress)
@@ -420,7 +424,6 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
     // wave-uniform block count (SGPR: scalar block-loop tests).
     const uint32_t max_l = wave_max(valid ? L : 0u);
     const uint32_t wave_nb = blocks_for_len(max_l);
-    if (b0 != 0u && b0 >= wave_nb) return kTileSkipped;  // wave-uniform (run lengths < plan lengths)
 
     // Bytes past arena_len inside the last dword are never part of a message
     // (they are masked by the padding logic), so the range rounds up to 4.
@@ -547,7 +550,7 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
         // branch inside it: two round copies joined inside the loop made the
         // register allocator spill (64 VGPRs is the 8-wave budget).
         const uint32_t loop_nb = tail_ok ? wave_nb - 1u : wave_nb;
-        if constexpr (kPf && !kDma) {
+        if constexpr (kPf && !kDma && !kDmaPipe) {
             if (far && aligned && b0 == 0u && finished) {
                 hash_tile_pipelined<kNoYield>(rsrc, vo, sel, L, min_l, uni, tail_ok, tw, wave_nb, loop_nb, nb, lane, my,
                                               st);
@@ -565,7 +568,7 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
         // Lane l of piece j fetches slot 64 j + l of the swizzled tile
         // (lds_slot's inverse), so the transposed read back is the loader's.
         bool dma = false;
-        if constexpr (kFused || kDma) dma = far && aligned;
+        if constexpr (kFused || kDma || kDmaPipe) dma = far && aligned;
         if (dma) {
             const uint32_t qd = (lane & 3u) ^ ((lane >> 4) & 3u);
             uint32_t vd[4];
@@ -573,6 +576,7 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
             for (int j = 0; j < 4; j++)
                 vd[j] = (uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) + 16u * qd;
             auto issue_dma = [&](uint32_t blk) {
+                if constexpr (kDiag == 1) return;
 #pragma unroll
                 for (int j = 0; j < 4; j++)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -584,8 +588,61 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
             const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
             const uint32_t d1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)loop_end);
             const uint32_t dmin = (uint32_t)__builtin_amdgcn_readfirstlane((int)min_l);
-            if (d0 < d1) issue_dma(d0);
-            for (uint32_t blk = d0; blk < d1; blk++) {
+            // kDmaPipe (A/B): block b+1's words are read back from LDS in the
+            // middle of block b's rounds (after statement 2; the wait for the
+            // reads after statement 4, then block b+2's DMA), so neither the
+            // DMA's landing nor the LDS round trip sits between two blocks.
+            // 16 more live VGPRs (the next block's words): CU-block kernel only.
+            auto read_words = [&](uint32_t x[16]) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the block landed in LDS
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint4 v = my[lds_slot(lane, (uint32_t)k)];
+                    x[4 * k + 0] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+                }
+            };
+            auto finish_words = [&](uint32_t blk, uint32_t x[16]) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) x[k] = __builtin_bswap32(x[k]);
+                if (64u * blk + 64u > dmin) {  // wave-uniform
+                    uint32_t wnb;  // (opaque copy, as below)
+                    asm volatile("s_mov_b32 %0, %1" : "=s"(wnb) : "s"(wave_nb));
+                    if (uni) {
+                        pad_block_uniform(x, 64u * blk, dmin, wnb - blk == 1u);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            pad_words(64u * blk + 16u * (uint32_t)k, L, blk + 1u == nb, (uint32_t)k, &x[4 * k]);
+                    }
+                }
+            };
+            if constexpr (kDmaPipe) {
+                if (d0 < d1) {
+                    uint32_t w[16];
+                    issue_dma(d0);
+                    read_words(w);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (d0 + 1u < d1) issue_dma(d0 + 1u);
+                    for (uint32_t blk = d0; blk < d1; blk++) {
+                        finish_words(blk, w);
+                        block_prio(blk);
+                        const bool next = blk + 1u < d1, next2 = blk + 2u < d1;  // wave-uniform
+                        uint32_t wn[16];
+                        compress_asm_hooked(st, w, blk < nb, [&](int k) {
+                            if (k == 2 && next) {
+                                read_words(wn);
+                            } else if (k == 4 && next) {
+                                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads back: free the tile
+                                if (next2) issue_dma(blk + 2u);
+                            }
+                        });
+#pragma unroll
+                        for (int i = 0; i < 16; i++) w[i] = wn[i];
+                    }
+                }
+            }
+            if (!kDmaPipe && d0 < d1) issue_dma(d0);
+            for (uint32_t blk = kDmaPipe ? d1 : d0; blk < d1; blk++) {
                 const uint32_t soff = 64u * blk;
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block blk landed in LDS
                 uint32_t w[16];
@@ -755,12 +812,18 @@ __global__ __launch_bounds__(64 * kMsgWaves, kWide ? 6 : kMsgOcc) void sha256_ms
 // in a 653 us launch (SQ_WAVE_CYCLES / SQ_WAVES, profiles/r03a), i.e. some
 // SIMDs ran 5-6 tiles while others idled.  Here each CU gets ONE workgroup of
 // 4k waves (kCuLds of LDS holds it alone on its CU), which the CU deals to
-// its SIMDs in cyclic order: exactly k waves per SIMD.  At k <= 4 a wave may
-// hold 128 VGPRs, so the next block's chunks are prefetched into registers.
+// its SIMDs in cyclic order: exactly k waves per SIMD.  Each wave's next
+// block lands in its LDS tile by DMA while this block's rounds run (kMode 0).
 constexpr uint32_t kCuLds = 96u * 1024u;
-// kMode: 0 = register-prefetching block loop (hash_tile_pipelined, the
-// product form), 1 = the same with no-yield rounds, 2 = the fused launch's
-// one-block-ahead LDS-DMA block loop (A/B forms, variants 11 and 12).
+// kMode: 0 = the product form: block b+1's loads issued as LDS-DMA
+// (buffer_load_dwordx4 ... lds) as soon as block b's words are read back,
+// the fused launch's loader (config 3 sequential plan, same box:
+// 0.632-0.634 vs 0.648 ms for the register-prefetching form, 1,424 vs
+// 1,443 VALU per compression, profiles/r04a, r04b); A/B forms: 1 = the
+// register-prefetching block loop (hash_tile_pipelined) with no-yield
+// rounds (variant 11), 2 = the same with the product rounds (round 3's
+// product form, variant 12), 3 = LDS-DMA with the next block's words read
+// back mid-block (variant 13: 0.638 ms, slower).
 template <int kMode>
 __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* __restrict__ arena,
                                                                  uint64_t arena_len,
@@ -773,8 +836,9 @@ __global__ __launch_bounds__(1024, 1) void sha256_msgs_cu_kernel(const uint8_t* 
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t t = blockIdx.x * (blockDim.x >> 6) + wv;
     if (t * 64u >= n) return;  // whole wave idle (wave-uniform)
-    hash_tile<true, false, false, true, kMode == 1, kMode == 2>(arena, arena_len, off, len, order, n, out,
-                                                                cu_lds + 256u * wv, t, lane);
+    hash_tile<true, false, false, true, kMode == 1, kMode == 0 || kMode >= 4, kMode == 3,
+              kMode == 4 ? 1 : kMode == 5 ? 2 : 0>(arena, arena_len, off, len, order, n, out, cu_lds + 256u * wv, t,
+                                                     lane);
 }
 
 // ---- overlapped cycles: this cycle's request tiles + the previous cycle's
@@ -1648,14 +1712,14 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // FusedArgs::test_placement (MIRSHA_AB=1 MIRSHA_TEST_PLACEMENT=remap)
     // makes every wave read SIMD 0, so the remap runs on real hardware.
     __shared__ uint32_t simd_waves[4];
-    __shared__ uint32_t extra_ticket;
+    __shared__ uint32_t extra_ticket, waves_counted;
     __shared__ uint32_t waves_retired;
     static_assert(kPacedRingOff + sizeof(FusedPairRing) <= kPacedLds && kPacedRingOff >= 4096u * kPacedMaxPace * 4u,
                   "paced LDS: staging tiles, then the pair ring");
     FusedPairRing& ring = *reinterpret_cast<FusedPairRing*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedRingOff);
     const bool list_block = blockIdx.x < a.list_waves;  // list_waves carries the number of LIST BLOCKS
     if (threadIdx.x < 4u) simd_waves[threadIdx.x] = 0u;
-    if (threadIdx.x == 0u) waves_retired = extra_ticket = 0u;
+    if (threadIdx.x == 0u) waves_retired = extra_ticket = waves_counted = 0u;
     if (threadIdx.x < 64u) g_bal_prog[threadIdx.x] = kBalDone;  // tile progress (kPrioBalance)
     if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = ring.aborted = 0u;
     __syncthreads();
@@ -1664,10 +1728,17 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     const uint32_t P = blockDim.x >> 8;
     uint32_t simd = a.test_placement ? 0u : (hw >> 4) & 3u;
     uint32_t slot = 0u;
-    if (lane == 0u) slot = atomicAdd(&simd_waves[simd], 1u);
+    if (lane == 0u) {
+        slot = atomicAdd(&simd_waves[simd], 1u);
+        __hip_atomic_fetch_add(&waves_counted, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     slot = (uint32_t)__shfl((int)slot, 0, 64);
-    __syncthreads();  // every wave counted
     if (slot >= P) {  // wave-uniform: an extra wave takes the next identity no wave holds
+        // Only extras wait for the whole block's count (no barrier: a block
+        // barrier here cost the fused config-3 step 0.80 -> 1.07 ms, profiles/r04d);
+        // every wave of the block is resident, so the count completes.
+        while (__hip_atomic_load(&waves_counted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u * P)
+            __builtin_amdgcn_s_sleep(1);
         uint32_t e = 0u;
         if (lane == 0u) e = atomicAdd(&extra_ticket, 1u);
         e = (uint32_t)__shfl((int)e, 0, 64);
@@ -1681,6 +1752,13 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             e -= miss;
         }
     }
+    // Scalar again (readfirstlane): the remap's LDS reads make the compiler
+    // treat simd / slot as per-lane values, and the roles derived from them
+    // (queue, issue priority) then turned into exec-mask branches -- every
+    // s_setprio of fixed_prio executed in turn, the queue priorities lost,
+    // the fused config-3 step 0.80 -> 1.07 ms (profiles/r04d, r04e).
+    simd = (uint32_t)__builtin_amdgcn_readfirstlane((int)simd);
+    slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot);
     bool own = true, tiles = true;
     if (list_block && (slot != 0u || simd > 1u)) {  // not the pair: a tile wave, or idle
         tiles = !(a.list_tiles == 0u || (a.list_tiles == 1u && simd <= 1u));
@@ -1782,15 +1860,26 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             // (inline, not wait_counter: a call here spilled the live tile state)
             bool ok = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0ull;
             const uint64_t target = a.seg_epoch * S + k_i, t0 = __builtin_amdgcn_s_memrealtime();
-            while (ok && !__shfl((int)(poll_counter(a.seg_flags + 16u * s_i) >= target), 0, 64)) {
+            uint32_t fin = 0u;  // the tile already finished (an earlier segment published the run's end)
+            while (ok) {
+                const uint64_t f = poll_counter(a.seg_flags + 16u * s_i);
+                if (__shfl((int)(f >= target), 0, 64)) {
+                    fin = (uint32_t)__shfl((int)(f >= a.seg_epoch * S + S), 0, 64);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(8);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > a.watchdog) {
                     if (lane == 0u) raise_error(a.err);
                     ok = false;
                 }
             }
-            if (!ok) {  // fail closed: this split tile's later segments and digest are never written
+            // fail closed: this split tile's later segments and digest are never written;
+            // fin: the run's messages are shorter than the plan's and an earlier
+            // segment stored the digest: nothing to do, nothing to publish
+            if (!ok || fin) {
                 seg = kNoSeg;
+#pragma unroll
+                for (int i = 0; i < 8; i++) st[i] = own_st[64 * i + lane];
                 continue;
             }
             if (b0) load_midstate_sc1(a.seg_state, s_i, lane, st);
@@ -1804,17 +1893,13 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
                  : a.tile_prio_progress     ? kPrioProgress
                                             : prio_of(a.steal_own_prio ? q : qq, a.n_queues);
         }
-        // (a segment's range is cut from the plan's lengths; with shorter
-        // messages at run time an earlier segment may already have finished
-        // the tile: this one is then kTileSkipped and only raises its flag)
-        const uint32_t rs = hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req,
-                                                         a.req_out, my, wt, lane, pr, b0, b1, st);
-        const bool done = rs == kTileDone;
-        if (rs == kTilePaused && !is_seg) {  // own tile paused at seg_at
+        const bool done = hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req,
+                                                       a.req_out, my, wt, lane, pr, b0, b1, st) == kTileDone;
+        if (!done && !is_seg) {  // own tile paused at seg_at
             ob0 = seg_at;
             continue;
         }
-        if (rs == kTilePaused) store_midstate_sc1(a.seg_state, s_i, lane, st);
+        if (!done) store_midstate_sc1(a.seg_state, s_i, lane, st);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (done) {
             if (!is_seg && a.trace && lane == 0) a.trace[3 * t + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1823,8 +1908,12 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
                 __hip_atomic_fetch_add(a.counters + a.tadj[j], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (is_seg) {
+            // segment done; a segment that finished the tile (the last, or an
+            // earlier one when the run's messages are shorter than the plan's
+            // cut) publishes the run's end, which the later segments skip on
             if (lane == 0u)
-                __hip_atomic_store(a.seg_flags + 16u * s_i, a.seg_epoch * a.seg_per_tile + k_i + 1u,
+                __hip_atomic_store(a.seg_flags + 16u * s_i,
+                                   a.seg_epoch * a.seg_per_tile + (done ? a.seg_per_tile : k_i + 1u),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             seg = kNoSeg;
 #pragma unroll
@@ -1991,11 +2080,11 @@ uint32_t cu_count() {
     return v;
 }
 
-// The dynamic-LDS limit of kernel `fn` (one of 5 forms) raised on the
+// The dynamic-LDS limit of kernel `fn` (one of 8 forms) raised on the
 // current device, once per (device, form): per-device flags, set with atomics
 // (mirsha_hash_batch_multi launches from one thread per device).
 hipError_t dyn_lds_attr(const void* fn, int form, uint32_t bytes) {
-    static std::atomic<uint8_t> done[64][5] = {};
+    static std::atomic<uint8_t> done[64][8] = {};
     int dev = 0;
     if (hipError_t e = hipGetDevice(&dev)) return e;
     if (dev >= 0 && dev < 64 && done[dev][form].load(std::memory_order_acquire)) return hipSuccess;
@@ -2023,21 +2112,31 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
-    if (variant == kVariantCu || variant == kVariantCuNoYield || variant == kVariantCuDma ||
+    if (variant == kVariantCu || variant == kVariantCuNoYield || variant == kVariantCuPrefetch || variant == kVariantCuDmaPipe || variant == kVariantCuDiagNoLoads ||
+        variant == kVariantCuDiagNoPrio ||
         (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
         // k waves per SIMD, one workgroup of 4k waves per CU
         const uint32_t k = (tiles + 4u * cu_count() - 1u) / (4u * cu_count());
         const uint32_t wg_waves = 4u * std::min(k, kCuMaxWavesPerSimd);
-        const int form = variant == kVariantCuNoYield ? 1 : variant == kVariantCuDma ? 2 : 0;
-        const void* fn = form == 1 ? (const void*)sha256_msgs_cu_kernel<1>
-                         : form == 2 ? (const void*)sha256_msgs_cu_kernel<2>
-                                     : (const void*)sha256_msgs_cu_kernel<0>;
-        if (hipError_t e = dyn_lds_attr(fn, form, kCuLds)) return e;
+        const int form = variant == kVariantCuNoYield ? 1 : variant == kVariantCuPrefetch ? 2
+                         : variant == kVariantCuDmaPipe ? 3 : variant == kVariantCuDiagNoLoads ? 4
+                         : variant == kVariantCuDiagNoPrio ? 5 : 0;
+        const void* fns[6] = {(const void*)sha256_msgs_cu_kernel<0>, (const void*)sha256_msgs_cu_kernel<1>,
+                              (const void*)sha256_msgs_cu_kernel<2>, (const void*)sha256_msgs_cu_kernel<3>,
+                              (const void*)sha256_msgs_cu_kernel<4>, (const void*)sha256_msgs_cu_kernel<5>};
+        const int slots[6] = {0, 1, 2, 5, 6, 7};  // dyn_lds_attr forms (3: fused, 4: placement probe)
+        if (hipError_t e = dyn_lds_attr(fns[form], slots[form], kCuLds)) return e;
         const uint32_t cgrid = (tiles + wg_waves - 1u) / wg_waves;
-        if (variant == kVariantCuNoYield)
+        if (form == 4)
+            sha256_msgs_cu_kernel<4><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+        else if (form == 5)
+            sha256_msgs_cu_kernel<5><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+        else if (form == 1)
             sha256_msgs_cu_kernel<1><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
-        else if (variant == kVariantCuDma)
+        else if (form == 2)
             sha256_msgs_cu_kernel<2><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+        else if (form == 3)
+            sha256_msgs_cu_kernel<3><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         else
             sha256_msgs_cu_kernel<0><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();

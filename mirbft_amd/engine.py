@@ -405,7 +405,8 @@ class Pipeline:
         self.handle = h
         self.mode = int(self._lib.mirsha_pipeline_mode(h))
         # 1: a fused plan built sequential after its placement probe (mirsha_pipeline_fallback)
-        self.fallback = int(self._lib.mirsha_pipeline_fallback(h))
+        self.fallback = int(self._lib.mirsha_pipeline_fallback(h)) if hasattr(self._lib, "mirsha_pipeline_fallback") \
+            else 0
         self.n_req = int(n_req)
         self.n_lists = int(fs.size) - 1
 
