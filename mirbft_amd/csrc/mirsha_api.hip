@@ -2655,7 +2655,16 @@ int mirsha_submit_slices_multi(mirsha_multi* m, const uint8_t* const* slice_ptr,
         return mirsha_submit_slices(m->ctx[k], slice_ptr + s0, slice_len + s0, firsts[k].data(), b - a,
                                     digests_out + 32ull * a, flags, &dt[k]);
     });
-    if (rc) return rc;
+    if (rc) {
+        // a device refused its range: retire the ranges the others queued
+        // before returning, so no digest lands in digests_out after the
+        // failed call (the caller may free it)
+        const std::string err = m->err;
+        for (size_t k = 0; k < dt.size(); k++)
+            if (dt[k]) (void)mirsha_wait(m->ctx[k], dt[k]);
+        m->err = err;
+        return rc;
+    }
     m->dev_tickets[(t - 1) % kMultiAsyncSlots] = dt;
     m->next_ticket++;
     *ticket_out = t;

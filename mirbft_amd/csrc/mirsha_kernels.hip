@@ -214,6 +214,7 @@ __device__ __forceinline__ void store_digest_sc1(__amdgpu_buffer_rsrc_t ors, uin
 // box-dependent.
 constexpr uint32_t kPrioTop = 3;
 __device__ __forceinline__ void progress_prio(uint32_t blk) {
+    blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)blk);  // scalar branches (see fixed_prio)
     const uint32_t p = blk < kPrioTop ? kPrioTop - blk : 0u;
     if (p >= 3u) __builtin_amdgcn_s_setprio(3);
     else if (p == 2u) __builtin_amdgcn_s_setprio(2);
@@ -228,7 +229,13 @@ __device__ __forceinline__ void progress_prio(uint32_t blk) {
 // Fixed issue priority of a fused-launch tile wave (its queue's), set before
 // each block's rounds in place of progress_prio.
 constexpr uint32_t kPrioProgress = 4;  // hash_tile<kFused>'s fprio: progress_prio instead of a fixed one
+// The priority is wave-uniform; readfirstlane keeps the branches below scalar.
+// When the compiler took it for a per-lane value, the branches became
+// exec-mask regions and more than one s_setprio could execute (s_setprio
+// ignores exec): fused config-3 runs then had some queue-0 waves at the
+// lowest priority, ending with queue 3 (profiles/r04f, tools/trace_queues.py).
 __device__ __forceinline__ void fixed_prio(uint32_t p) {
+    p = (uint32_t)__builtin_amdgcn_readfirstlane((int)p);
     if (p >= 3u) __builtin_amdgcn_s_setprio(3);
     else if (p == 2u) __builtin_amdgcn_s_setprio(2);
     else if (p == 1u) __builtin_amdgcn_s_setprio(1);
@@ -1732,33 +1739,35 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
         slot = atomicAdd(&simd_waves[simd], 1u);
         __hip_atomic_fetch_add(&waves_counted, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    slot = (uint32_t)__shfl((int)slot, 0, 64);
-    if (slot >= P) {  // wave-uniform: an extra wave takes the next identity no wave holds
-        // Only extras wait for the whole block's count (no barrier: a block
-        // barrier here cost the fused config-3 step 0.80 -> 1.07 ms, profiles/r04d);
-        // every wave of the block is resident, so the count completes.
-        while (__hip_atomic_load(&waves_counted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4u * P)
+    // Everything below is scalar (readfirstlane on every LDS-read value): a
+    // remap written with per-lane values made the compiler treat the whole
+    // identity as divergent, and with this block present -- never executed
+    // -- the fused config-3 step went 0.80 -> 1.07 ms (profiles/r04d-r04f
+    // bisected it to this block).
+    slot = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)slot, 0, 64));
+    if (slot >= P) {  // scalar branch: an extra wave takes the next identity no wave holds
+        // Only extras wait for the whole block's count (no barrier): every
+        // wave of the block is resident, so the count completes.
+        while ((uint32_t)__builtin_amdgcn_readfirstlane((int)__hip_atomic_load(
+                   &waves_counted, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 4u * P)
             __builtin_amdgcn_s_sleep(1);
         uint32_t e = 0u;
         if (lane == 0u) e = atomicAdd(&extra_ticket, 1u);
-        e = (uint32_t)__shfl((int)e, 0, 64);
+        e = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)e, 0, 64));
+        uint32_t ns = simd, nsl = slot;
         for (uint32_t s4 = 0; s4 < 4u; s4++) {
-            const uint32_t have = min(simd_waves[s4], P), miss = P - have;
+            const uint32_t have = min((uint32_t)__builtin_amdgcn_readfirstlane((int)simd_waves[s4]), P);
+            const uint32_t miss = P - have;
             if (e < miss) {
-                simd = s4;
-                slot = have + e;
+                ns = s4;
+                nsl = have + e;
                 break;
             }
             e -= miss;
         }
+        simd = ns;
+        slot = nsl;
     }
-    // Scalar again (readfirstlane): the remap's LDS reads make the compiler
-    // treat simd / slot as per-lane values, and the roles derived from them
-    // (queue, issue priority) then turned into exec-mask branches -- every
-    // s_setprio of fixed_prio executed in turn, the queue priorities lost,
-    // the fused config-3 step 0.80 -> 1.07 ms (profiles/r04d, r04e).
-    simd = (uint32_t)__builtin_amdgcn_readfirstlane((int)simd);
-    slot = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot);
     bool own = true, tiles = true;
     if (list_block && (slot != 0u || simd > 1u)) {  // not the pair: a tile wave, or idle
         tiles = !(a.list_tiles == 0u || (a.list_tiles == 1u && simd <= 1u));
@@ -1838,7 +1847,9 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
                     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
                     a.trace[3 * t] = __builtin_amdgcn_s_memrealtime();
                     a.trace[3 * t + 2] = (unsigned long long)hw | ((unsigned long long)(xcc & 0xFFu) << 32) |
-                                         ((unsigned long long)qq << 40) | ((unsigned long long)slot << 44);
+                                         ((unsigned long long)qq << 40) | ((unsigned long long)slot << 44) |
+                                         ((unsigned long long)simd << 48) |
+                                         ((unsigned long long)(list_block ? 1u : 0u) << 52);
                 }
             }
         }

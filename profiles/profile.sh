@@ -15,7 +15,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-r02}
 shift || true
 ARGS=("--gpus" "1" "--steps" "20" "--warmup" "5" "$@")
-PARGS=("${ARGS[@]}" "--cpu-seconds" "0" "--no-pcie")
+PARGS=("${ARGS[@]}" "--cpu-seconds" "0" "--no-pcie" "--no-config3-leg")
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 bench.py "${ARGS[@]}" > "$OUT/bench_under_trace.jsonl" 2> "$OUT/trace.err"

@@ -21,9 +21,15 @@ done
 done
 unset MIRSHA_AB_LIB
 export MIRSHA_AB=1
+k=0
 for v in 0 12 14 15 0; do
-timeout -k 10 300 python -u bench.py --config 3 --pipeline sequential --variant $v --steps 20 --warmup 5 --cpu-seconds 0 --no-pcie --no-overlap-extra > $O/c3seq_v$v.jsonl 2>> $O/err.txt || { tail $O/err.txt; exit 1; }
-show $O/c3seq_v$v.jsonl
+k=$((k+1))
+MIRSHA_PROBE_WAVES=4 timeout -k 10 300 python -u bench.py --config 3 --pipeline sequential --variant $v --steps 20 --warmup 5 --cpu-seconds 0 --no-pcie --no-overlap-extra > $O/c3seq_v$v.$k.jsonl 2>> $O/err.txt || { tail $O/err.txt; exit 1; }
+show $O/c3seq_v$v.$k.jsonl
+python3 -c "
+import json
+d=json.loads(open('$O/c3seq_v$v.$k.jsonl').readlines()[-1]); m=d['roofline']['measured_peak']
+print('   probe(4 waves/SIMD) cycles/wave-compression', round(m['cycles_per_wave_compression']), 'kernel frac of probe', round(m['frac'],3))"
 done
 unset MIRSHA_AB
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "split or placement or fused or overlap or config3 or cu" -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }

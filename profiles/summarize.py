@@ -20,7 +20,8 @@ import sys
 
 
 def short(name):
-    for k in ("clock_probe_kernel", "sha256_msgs_overlap_kernel", "sha256_msgs_kernel", "sha256_lists_kernel", "sha256_chain_kernel",
+    for k in ("clock_probe_kernel", "sha256_msgs_overlap_kernel", "sha256_msgs_cu_kernel", "sha256_msgs_kernel",
+              "sha256_lists_kernel", "sha256_chain_kernel",
               "sha256_chain_pair_kernel", "sha256_fused_paced_kernel",
               "gen_requests_kernel", "gen_mixed_kernel"):
         if k in name:

@@ -27,11 +27,14 @@ def main():
     p.add_argument("--config", type=int, default=2)
     p.add_argument("--variant", type=int, default=0)
     p.add_argument("--kernel", default="sha256_msgs_kernel")
+    p.add_argument("--from-kernel", default=None,
+                   help="summary entry to read (default --kernel); e.g. sha256_msgs_cu_kernel, the form "
+                        "launch_msgs picks for 1,025-4,096 tiles, which bench.py reports as sha256_msgs_kernel")
     p.add_argument("--algorithmic", type=float, default=None, help="algorithmic bytes per launch (for the ratio)")
     a = p.parse_args()
     from bench import kernel_source_key  # noqa: E402
 
-    k = json.load(open(a.summary))["kernels"][a.kernel]
+    k = json.load(open(a.summary))["kernels"][a.from_kernel or a.kernel]
     entry = {
         "key": kernel_source_key(a.variant), "config": a.config, "variant": a.variant, "kernel": a.kernel,
         "hbm_bytes_per_launch": k["hbm_bytes_per_launch"],

@@ -229,6 +229,21 @@ def case_split(eng, rng, seed):
         plan.status()
         check(np.array_equal(d_req[0].cpu().numpy(), want), tag + ": requests", seed)
         check(np.array_equal(d_lst.cpu().numpy()[:nl], want_l), tag + ": lists", seed)
+    # a run whose lengths differ from the plan's (prefixes of the planned
+    # messages: split-tile segments past a tile's end are skipped), then the
+    # planned lengths again on the same plan
+    short = (ln // int(rng.integers(2, 6))).astype(np.uint32)
+    want_s = oracle_py.hash_requests(arena, off, short, threads=8)
+    d_len_s = torch.from_numpy(short.view(np.int32)).cuda()
+    d_req[1].zero_()
+    d_lst.zero_()
+    torch.cuda.synchronize()
+    eng.hash_requests_then_batches_device(plan, d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len_s.data_ptr(),
+                                          d_req[1].data_ptr(), d_lst.data_ptr())
+    plan.status()
+    check(np.array_equal(d_req[1].cpu().numpy(), want_s), tag + ": short-run requests", seed)
+    check(np.array_equal(d_lst.cpu().numpy()[:nl], oracle_py.batch_digests(want_s, idx, first)),
+          tag + ": short-run lists", seed)
     for i in range(3):
         prev = d_req[(i + 1) % 2].data_ptr() if i else 0
         d_lst.zero_()
@@ -278,22 +293,56 @@ def case_chains(eng, rng, seed):
     ch.close()
 
 
+def case_multi(multi, rng, seed):
+    """The multi-device drop-in (two contexts on device 0): slices with empty
+    requests and empty slices, sync and async (with and without dedup)."""
+    from mirbft_amd import SliceArrays
+
+    n = int(rng.integers(1, 30000))
+    ln = lengths(rng, n)
+    arena, off = arena_for(rng, ln)
+    base = arena.ctypes.data
+    # 1-3 slices per request, cut at random points inside each message
+    k = rng.integers(1, 4, n)
+    ptr, sl, first = [], [], [0]
+    for i in range(n):
+        cuts = np.sort(rng.integers(0, int(ln[i]) + 1, int(k[i]) - 1)) if k[i] > 1 else np.zeros(0, np.int64)
+        bounds = [0] + [int(c) for c in cuts] + [int(ln[i])]
+        for a, b in zip(bounds, bounds[1:]):
+            ptr.append(base + int(off[i]) + a)
+            sl.append(b - a)
+        first.append(len(ptr))
+    arrays = SliceArrays(np.array(ptr, np.uint64), np.array(sl, np.uint64), np.array(first, np.uint32), keep=(arena,))
+    want = oracle_py.hash_requests(arena, off, ln, threads=8)
+    if rng.random() < 0.5:
+        check(np.array_equal(multi.hash_slice_arrays(arrays), want), f"multi sync n={n}", seed)
+    else:
+        t = multi.submit_slices(arrays, dedup=bool(rng.random() < 0.5))
+        check(np.array_equal(multi.wait(t), want), f"multi async n={n}", seed)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
     ap.add_argument("--seed", type=int, default=1)
     a = ap.parse_args()
+    from mirbft_amd import MultiEngine
+
     eng = Engine(0)
+    multi = MultiEngine([0, 0])
     t0 = last = time.time()
-    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0, "chains": 0, "split": 0}
+    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0, "chains": 0, "split": 0, "multi": 0}
     k = 0
     while time.time() - t0 < a.seconds:
         seed = a.seed * 1_000_003 + k
         rng = np.random.default_rng(seed)
-        which = ("host", "slices", "plan", "host", "slices", "plan", "large", "chains", "split")[k % 9]
+        which = ("host", "slices", "plan", "host", "slices", "plan", "large", "chains", "split", "multi")[k % 10]
         try:
-            {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large,
-             "chains": case_chains, "split": case_split}[which](eng, rng, seed)
+            if which == "multi":
+                case_multi(multi, rng, seed)
+            else:
+                {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large,
+                 "chains": case_chains, "split": case_split}[which](eng, rng, seed)
         except AssertionError as e:
             print(e, flush=True)
             sys.exit(1)
@@ -302,6 +351,7 @@ def main():
         if time.time() - last > 15:
             print(f"{time.time() - t0:.0f} s: {counts}", flush=True)
             last = time.time()
+    multi.close()
     eng.close()
     print(f"soak ok: {k} cases in {time.time() - t0:.0f} s {counts}", flush=True)
 

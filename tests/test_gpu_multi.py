@@ -135,3 +135,18 @@ def test_hash_arena_multi(multi, pinned):
     assert np.array_equal(got, oracle_py.hash_requests(src, off, lens, threads=8))
     cut = multi.last_cut()
     assert cut[0] == 0 and cut[-1] == n and 0 < cut[1] < n
+
+
+def test_async_multi_error_retires_other_ranges(multi):
+    """A submission one device refuses (a NULL slice with bytes in the second
+    range) fails with EINVAL after the other device's range has been
+    retired; the multi context stays usable."""
+    reqs = _requests(40, 6000)
+    sl = SliceArrays.from_requests(reqs)
+    bad = sl.ptr.copy()
+    bad[int(np.flatnonzero(sl.len)[-5])] = 0
+    with pytest.raises(MirshaError) as e:
+        multi.submit_slices(SliceArrays(bad, sl.len, sl.first, keep=(sl,)))
+    assert e.value.code == _lib.MIRSHA_EINVAL
+    t = multi.submit_slices(sl)
+    assert np.array_equal(multi.wait(t), _want(reqs))
