@@ -75,3 +75,18 @@ def test_no_gpu_context_is_an_error_not_a_fallback():
 
     with pytest.raises(MirshaError):
         Engine(0)
+
+
+def test_no_gpu_multi_is_an_error_not_a_fallback():
+    """The multi-device drop-in has no CPU path either: without a device the
+    context set is refused, and bad device lists are refused up front."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("has a GPU")
+    from mirbft_amd import MirshaError, MultiEngine
+
+    with pytest.raises(MirshaError):
+        MultiEngine([0])
+    with pytest.raises(MirshaError):
+        MultiEngine([])
