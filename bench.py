@@ -41,7 +41,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from mirbft_amd import Engine, sharding  # noqa: E402
+from mirbft_amd import Engine, MultiEngine, sharding  # noqa: E402
 from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS, KERNEL_OVERLAP  # noqa: E402
 
 SEED_BASE = 0x6D69726266740000
@@ -326,6 +326,63 @@ class BatchWorkload:
                 "pinned_arena": {"digests_per_s": self.digests / qdt, "gb_per_s": self.bytes_hashed / qdt / 1e9,
                                  "ms_per_call": qdt * 1e3, "calls_ms": qcalls, "host_phases_ms": qprof,
                                  "note": "the same call on an arena from mirsha_host_alloc (page-locked)"}}
+
+    def multi_device(self):
+        """The multi-GPU drop-in (mirsha_hash_arena_multi, INTEGRATION.md's
+        GPUHasherMulti): the config's requests from host memory, cut into
+        contiguous ranges of equal bytes, one per listed device, each over its
+        own PCIe link and stream.  Devices: every visible GPU when there are
+        several, else two contexts on GPU 0 (one link: the mechanics and the
+        per-device phases, not a speed-up).  Digests checked against the
+        oracle on samples at both ends and on both sides of every cut."""
+        ndev = torch.cuda.device_count()
+        devices = list(range(ndev)) if ndev > 1 else [0, 0]
+        n, stride = self.n, self.stride
+        arena_h = self.d_arena.cpu().numpy()
+        off_h = np.arange(n, dtype=np.uint64) * stride
+        len_h = np.full(n, stride, dtype=np.uint32)
+        out = np.empty((n, 32), dtype=np.uint8)
+        m = MultiEngine(devices)
+        try:
+            m.set_variant(self.a.variant)
+
+            def rate(arena):
+                m.hash_arena(arena, off_h, len_h, out=out)  # warm device buffers
+                t = []
+                for _ in range(5):
+                    t1 = time.perf_counter()
+                    m.hash_arena(arena, off_h, len_h, out=out)
+                    t.append(time.perf_counter() - t1)
+                return float(np.median(t)), [round(x * 1e3, 3) for x in t]
+
+            pdt, pcalls = rate(arena_h)
+            pinned = m.host_empty(arena_h.size)
+            pinned[:] = arena_h
+            qdt, qcalls = rate(pinned)
+            cut = m.last_cut()
+            # oracle samples: the first and last requests and both sides of every cut
+            o, k = _oracle(), 128
+            starts = sorted({0, max(n - k, 0)} | {min(max(c - k // 2, 0), max(n - k, 0)) for c in cut[1:-1]})
+            ok = True
+            for i0 in starts:
+                cnt = min(k, n - i0)
+                sample = o.gen_requests(self.seed, self.first_req + i0, cnt, self.data_len)
+                want = o.hash_requests(sample, np.arange(cnt, dtype=np.uint64) * stride, np.full(cnt, stride))
+                ok = ok and bool(np.array_equal(out[i0:i0 + cnt], want))
+            phases = [{"device": d, "requests": cut[k + 1] - cut[k], "host_phases_ms": m.host_profile(k)}
+                      for k, d in enumerate(devices)]
+        finally:
+            m.close()
+        req_bytes = n * stride
+        return {"devices": devices, "digests_per_s": n / qdt, "gb_per_s": req_bytes / qdt / 1e9,
+                "ms_per_call": qdt * 1e3, "calls_ms": qcalls, "per_device": phases,
+                "pageable": {"digests_per_s": n / pdt, "gb_per_s": req_bytes / pdt / 1e9, "ms_per_call": pdt * 1e3,
+                             "calls_ms": pcalls},
+                "self_check": ok,
+                "note": "mirsha_hash_arena_multi, request digests only (no lists), page-locked arena from "
+                        "mirsha_multi_host_alloc (headline) and pageable; median of 5 calls after a warm-up; "
+                        "per_device = the last pinned call's range and phases per device context"
+                        + ("" if ndev > 1 else "; one GPU visible: two contexts share its link")}
 
     def cgo_path(self):
         """The Go binding's HashBatch end to end, slices -> digests
@@ -876,6 +933,12 @@ def main():
     # device-resident steps.
     pcie = wl.pcie() if rank == 0 and world == 1 and not a.no_pcie else None
     cgo = wl.cgo_path() if rank == 0 and world == 1 and not a.no_pcie and hasattr(wl, "cgo_path") else None
+    multi = None
+    if rank == 0 and world == 1 and not a.no_pcie and a.config == 2 and hasattr(wl, "multi_device"):
+        try:  # an extra leg: a failure is reported in the line, not fatal to it
+            multi = wl.multi_device()
+        except Exception as e:  # noqa: BLE001
+            multi = {"error": f"{type(e).__name__}: {e}"}
     torch.cuda.synchronize(dev)
 
     for _ in range(a.warmup):
@@ -1050,6 +1113,7 @@ def main():
                             "data_path_collectives": "none: each rank hashes its own request range; "
                                                      "barriers and max / sum reductions of timings only"},
             "pcie_inclusive": pcie,
+            "multi_device": multi,
             "cgo_path": cgo,
             "config3": c3,
             "cpu_baseline": cpu,
