@@ -115,6 +115,20 @@ def test_single_device_list_and_errors():
     m.close()
 
 
+@pytest.mark.parametrize("n", [3, 9000])
+def test_four_contexts(n):
+    """Four device contexts (the cut, the rebased lists and the gather over
+    more ranges than the paired tests); n = 3 leaves a range empty."""
+    m = MultiEngine([0, 0, 0, 0])
+    reqs = _requests(60 + n, n)
+    assert np.array_equal(m.hash_slices(reqs), _want(reqs))
+    cut = m.last_cut()
+    assert len(cut) == 5 and cut[0] == 0 and cut[-1] == n and cut == sorted(cut)
+    t = m.submit_slices(reqs)
+    assert np.array_equal(m.wait(t), _want(reqs))
+    m.close()
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_hash_arena_multi(multi, pinned):
     """mirsha_hash_arena_multi (the Go GPUHasherMulti's call): one arena,
