@@ -1285,6 +1285,14 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_OVERLAP_PRIO"))
         if (overlap) a.tile_prio_progress = strcmp(e, "queue") == 0 ? 0u : strcmp(e, "progress") == 0 ? 1u : 2u;
     a.test_placement = p->test_placement;
+    // A tile wave left alone on its SIMD runs the latency round form
+    // (FusedArgs::lone_form).  A/B: MIRSHA_FUSED_LONE_FORM=0.
+    a.lone_form = 1u;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_LONE_FORM")) a.lone_form = atoi(e) != 0 ? 1u : 0u;
+    // The last queue's tile waves stage two blocks ahead (FusedArgs::deep_last).
+    // A/B: MIRSHA_FUSED_DEEP_LAST=0.
+    a.deep_last = 1u;
+    if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_DEEP_LAST")) a.deep_last = atoi(e) != 0 ? 1u : 0u;
     a.seg_nb = p->d_seg_nb.as<uint32_t>();
     a.seg_state = p->d_seg_state.as<uint32_t>();
     a.seg_flags = p->d_seg_flags.as<unsigned long long>();

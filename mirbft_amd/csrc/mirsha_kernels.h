@@ -171,6 +171,13 @@ struct FusedArgs {
     // Test only (MIRSHA_AB=1 MIRSHA_TEST_PLACEMENT=remap): every wave reads
     // SIMD 0, so the in-kernel identity remap of a non-cyclic placement runs.
     uint32_t test_placement;
+    // Tile waves switch to the latency round form (no issue yields) while they
+    // are the only live wave of their SIMD (sha256_fused_paced_kernel; A/B:
+    // MIRSHA_FUSED_LONE_FORM=0 keeps the throughput form throughout).
+    uint32_t lone_form;
+    // The last queue's waves of the tile blocks keep two blocks of loads in
+    // flight (A/B: MIRSHA_FUSED_DEEP_LAST=0 keeps one).
+    uint32_t deep_last;
     unsigned long long seg_epoch;
     const uint32_t* seg_nb;            // blocks of each split tile
     uint32_t* seg_state;
@@ -182,6 +189,10 @@ struct FusedArgs {
 // tile waves per SIMD.
 constexpr uint32_t kPacedRingOff = 64u * 1024u;
 constexpr uint32_t kPacedLds = 97u * 1024u;
+// Tile blocks: the last queue's second staging tiles (4 KiB per SIMD) after
+// the parked midstates (2 KiB per SIMD at kPacedRingOff).
+constexpr uint32_t kPacedDeepOff = kPacedRingOff + 8u * 1024u;
+static_assert(kPacedDeepOff + 4u * 4096u <= kPacedLds, "paced LDS: deep staging tiles");
 constexpr uint32_t kPacedMaxPace = 4;
 hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, hipStream_t s);
 // Placement probe of the fused launch's block shape: *broken |= 1 when some

@@ -260,6 +260,19 @@ constexpr uint32_t kBalDone = 0xFFFFFFFFu;
 // s_getreg where needed, so no register stays live across the block loop of
 // the fused kernel, which sits at its 128-VGPR budget).
 __shared__ uint32_t g_bal_prog[4 * 16];
+
+// Live waves per SIMD of a fused-launch workgroup (set to the waves per SIMD
+// at launch, decremented as each wave leaves).  A tile wave that finds itself
+// the only one left runs its blocks in the latency round form: the issue
+// yields of the throughput form only stall a lone wave (tools/ilp_asm_probe,
+// profiles/r04k: 7,424 vs 5,991 cycles per compression at one wave per SIMD,
+// 5,314 vs 5,607 at four).
+__shared__ uint32_t g_simd_live[4];
+__device__ __forceinline__ bool simd_alone(uint32_t sel) {  // sel = SIMD + 1 (0: never)
+    if (sel == 0u) return false;
+    const uint32_t n = __hip_atomic_load(&g_simd_live[sel - 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)n) <= 1u;
+}
 __device__ __forceinline__ uint32_t bal_word() {
     uint32_t hw;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -394,7 +407,9 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
                                           const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                           const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ out,
                                           uint4* my, uint32_t t, uint32_t lane, uint32_t fprio = 0,
-                                          uint32_t b0 = 0u, uint32_t b1 = 0xFFFFFFFFu, uint32_t* st_io = nullptr) {
+                                          uint32_t b0 = 0u, uint32_t b1 = 0xFFFFFFFFu, uint32_t* st_io = nullptr,
+                                          uint32_t lone_sel = 0u, uint4* my2 = nullptr,
+                                          unsigned long long* lone_tr = nullptr) {
     auto block_prio = [&](uint32_t blk) {
         if constexpr (kDiag == 2) {
             return;
@@ -582,12 +597,19 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
 #pragma unroll
             for (int j = 0; j < 4; j++)
                 vd[j] = (uint32_t)__shfl((int)(uint32_t)o, 16 * j + (int)(lane >> 2), 64) + 16u * qd;
+            // Two blocks in flight (kFused, my2 != nullptr: the last queue's
+            // waves, which end their tiles alone on the SIMD, where one block
+            // of lead did not cover the load latency): block b lands in tile
+            // b & 1 (my, my2) and block b + 2's DMA follows b's read-back.
+            const bool deep = kFused && my2 != nullptr;  // wave-uniform
+            auto tile_of = [&](uint32_t blk) { return (deep && (blk & 1u)) ? my2 : my; };
             auto issue_dma = [&](uint32_t blk) {
                 if constexpr (kDiag == 1) return;
+                uint4* t = tile_of(blk);
 #pragma unroll
                 for (int j = 0; j < 4; j++)
                     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                        rsrc, (__attribute__((address_space(3))) void*)(my + 64 * j), 16, vd[j], 64u * blk, 0, 0);
+                        rsrc, (__attribute__((address_space(3))) void*)(t + 64 * j), 16, vd[j], 64u * blk, 0, 0);
             };
             // (bounds through readfirstlane: the block index is the DMA's
             // scalar offset, and a bound the compiler takes for divergent
@@ -648,19 +670,27 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
                     }
                 }
             }
-            if (!kDmaPipe && d0 < d1) issue_dma(d0);
+            if (!kDmaPipe && d0 < d1) {
+                issue_dma(d0);
+                if (deep && d0 + 1u < d1) issue_dma(d0 + 1u);
+            }
             for (uint32_t blk = kDmaPipe ? d1 : d0; blk < d1; blk++) {
                 const uint32_t soff = 64u * blk;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // block blk landed in LDS
+                // block blk landed in LDS (deep: block blk + 1's 4 loads may stay in flight)
+                if (deep && blk + 1u < d1)
+                    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 uint32_t w[16];
+                const uint4* tb = tile_of(blk);
 #pragma unroll
                 for (int k = 0; k < 4; k++) {
-                    const uint4 x = my[lds_slot(lane, (uint32_t)k)];
+                    const uint4 x = tb[lds_slot(lane, (uint32_t)k)];
                     w[4 * k + 0] = x.x; w[4 * k + 1] = x.y; w[4 * k + 2] = x.z; w[4 * k + 3] = x.w;
                 }
                 // the reads are back before the next DMA overwrites the tile
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (blk + 1u < d1) issue_dma(blk + 1u);
+                if (blk + (deep ? 2u : 1u) < d1) issue_dma(blk + (deep ? 2u : 1u));
 #pragma unroll
                 for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(w[k]);
                 if (soff + 64u > dmin) {  // wave-uniform
@@ -675,7 +705,20 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
                     }
                 }
                 block_prio(blk);
-                if (blk < nb) compress_asm(st, w);
+                if constexpr (kFused) {
+                    // the SIMD's only live wave: latency round form (g_simd_live)
+                    if (simd_alone(lone_sel)) {  // wave-uniform
+                        if (lone_tr != nullptr) {  // traced runs: the first lone block (bits 53..62, flag 63)
+                            if (lane == 0u) *lone_tr |= 1ull << 63 | (unsigned long long)min(blk, 1023u) << 53;
+                            lone_tr = nullptr;
+                        }
+                        if (blk < nb) compress_asm_lat(st, w);
+                    } else if (blk < nb) {
+                        compress_asm(st, w);
+                    }
+                } else if (blk < nb) {
+                    compress_asm(st, w);
+                }
             }
         }
         for (uint32_t blk = dma ? loop_end : b0; blk < loop_end; blk++) {
@@ -1728,6 +1771,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     if (threadIdx.x < 4u) simd_waves[threadIdx.x] = 0u;
     if (threadIdx.x == 0u) waves_retired = extra_ticket = waves_counted = 0u;
     if (threadIdx.x < 64u) g_bal_prog[threadIdx.x] = kBalDone;  // tile progress (kPrioBalance)
+    if (threadIdx.x < 4u) g_simd_live[threadIdx.x] = blockDim.x >> 8;  // P live waves per SIMD
     if (list_block && threadIdx.x == 0u) ring.produced = ring.consumed = ring.aborted = 0u;
     __syncthreads();
     uint32_t hw;
@@ -1821,6 +1865,11 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // A host's own tile's midstate while it runs its segment: in the tile
     // block's unused pair-ring LDS (2 KiB per SIMD's host wave), not registers.
     uint32_t* own_st = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedRingOff) + 512u * simd;
+    // The last queue's waves of a tile block stage two blocks ahead (hash_tile
+    // my2): a second 4 KiB tile per SIMD after the parked midstates.
+    uint4* deep_tile = (a.deep_last && !list_block && slot == last)
+                           ? reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(paced_lds) + kPacedDeepOff) + 256u * simd
+                           : nullptr;
     while (true) {
         if (!have && tiles) {
             qq = own ? q : last;
@@ -1905,7 +1954,10 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
                                             : prio_of(a.steal_own_prio ? q : qq, a.n_queues);
         }
         const bool done = hash_tile<true, false, true>(a.arena, a.arena_len, a.off, a.len, a.order, a.n_req,
-                                                       a.req_out, my, wt, lane, pr, b0, b1, st) == kTileDone;
+                                                       a.req_out, my, wt, lane, pr, b0, b1, st,
+                                                       (a.lone_form && slot == last) ? simd + 1u : 0u, deep_tile,
+                                                       (a.trace && !is_seg) ? a.trace + 3 * t + 2 : nullptr) ==
+                          kTileDone;
         if (!done && !is_seg) {  // own tile paused at seg_at
             ob0 = seg_at;
             continue;
@@ -1934,6 +1986,8 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
             if (lane == 0u) balance_done();  // no longer behind anyone (kPrioBalance)
         }
     }
+    // this wave is no longer live on its SIMD (g_simd_live: a tile wave left alone switches round forms)
+    if (lane == 0u) __hip_atomic_fetch_sub(&g_simd_live[simd], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     fused_retire(a.ctl, lane, &waves_retired);
 }
 

@@ -2,7 +2,7 @@
 """One traced fused config-3 run (GPU box): per tile queue, how many tiles,
 which wave slots served them, and their end-time quantiles (us from the
 first tile start); the list chunks' readiness-pass times.  Compare builds
-with MIRSHA_AB_LIB.  Usage: trace_queues.py"""
+with MIRSHA_AB_LIB.  Usage: trace_queues.py [requests]"""
 import os
 
 os.environ["MIRSHA_AB"] = "1"
@@ -20,7 +20,8 @@ from mirbft_amd import Engine, sharding  # noqa: E402
 def main():
     dev = torch.device("cuda", 0)
     eng = Engine(0)
-    n, data_len, bs = 1 << 18, 4096, 500
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 18  # requests (64 per tile)
+    data_len, bs = 4096, 500
     stride = 16 + data_len
     d_arena = torch.empty(n * stride, dtype=torch.uint8, device=dev)
     eng.synth_requests_device(0x6D69726266740003, 0, n, data_len, d_arena.data_ptr())
@@ -64,6 +65,31 @@ def main():
             print(f"  late q{qq} tile {i}: start {start[i]:.0f} end {end[i]:.0f} us, hw simd {(hw >> 4) & 3} wave "
                   f"{hw & 15} cu {(hw >> 8) & 15} sh {(hw >> 12) & 1} se {(hw >> 13) & 7} xcc {(int(info[i]) >> 32) & 0xFF}"
                   f" slot {int(slot[i])} identity simd {int(isimd[i])} list block {int(lb[i])}")
+    lone = ok & (info < 0)  # bit 63: the tile ran blocks as its SIMD's only live wave (from bit 53..62's block)
+    if lone.any():
+        lb0 = (info >> 53) & 0x3FF
+        print(f"lone-wave tiles: {int(lone.sum())}, first lone block p10/50/90 "
+              f"{np.percentile(lb0[lone], [10, 50, 90]).tolist()}")
+        # per physical SIMD: the lone stretch starts when the SIMD's other tile
+        # waves end (their tiles' ends), so a lone tile's block time is
+        # (its end - that) / (blocks left after its first lone block)
+        hwv = info & 0xFFFFFFFF
+        loc = ((info >> 32) & 0xFF) * 4096 + ((hwv >> 13) & 7) * 512 + ((hwv >> 12) & 1) * 256 + ((hwv >> 8) & 15) * 16 \
+            + ((hwv >> 4) & 3)
+        other_end = {}
+        for i in np.flatnonzero(ok & ~lone):
+            other_end[int(loc[i])] = max(other_end.get(int(loc[i]), 0.0), float(end[i]))
+        rates = []
+        for i in np.flatnonzero(lone):
+            t_alone = other_end.get(int(loc[i]))
+            left = 65 - int(lb0[i])
+            if t_alone is not None and left >= 8 and end[i] > t_alone:
+                rates.append((end[i] - t_alone) / left)
+        if rates:
+            print(f"lone stretch us per block (config-3 tiles, >= 8 blocks left): n {len(rates)}, p10/50/90 "
+                  f"{np.round(np.percentile(rates, [10, 50, 90]), 2).tolist()}")
+    else:
+        print("lone-wave tiles: none")
     passed = (tr[3 * nt: 3 * nt + nc] - t0) / 100.0
     print("readiness chunks passed p10/50/90/max us:", [round(float(np.percentile(passed, p)), 0) for p in (10, 50, 90, 100)])
     gend = (tr[3 * nt + nc: 3 * nt + nc + ng] - t0) / 100.0
