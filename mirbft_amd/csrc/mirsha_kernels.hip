@@ -261,6 +261,22 @@ constexpr uint32_t kBalDone = 0xFFFFFFFFu;
 // the fused kernel, which sits at its 128-VGPR budget).
 __shared__ uint32_t g_bal_prog[4 * 16];
 
+// An LDS word read through inline asm: for an ordinary (or atomic) LDS
+// access the compiler cannot prove distinct from a tile the wave's LDS-DMA is
+// still filling, so it waits for every outstanding vector-memory op first
+// (s_waitcnt vmcnt(0)), i.e. for the DMA of the next block(s) -- which turned
+// the loads' prefetch into a full memory round trip per block (a lone wave:
+// +750 cycles per block, tools/lone_probe.hip mode 7, profiles/r04l).  The
+// word is never a DMA target; only the wave's own LDS ops are waited for.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint32_t lds_load_nodma(const uint32_t* p) {
+    uint32_t v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
+
 // Live waves per SIMD of a fused-launch workgroup (set to the waves per SIMD
 // at launch, decremented as each wave leaves).  A tile wave that finds itself
 // the only one left runs its blocks in the latency round form: the issue
@@ -270,7 +286,7 @@ __shared__ uint32_t g_bal_prog[4 * 16];
 __shared__ uint32_t g_simd_live[4];
 __device__ __forceinline__ bool simd_alone(uint32_t sel) {  // sel = SIMD + 1 (0: never)
     if (sel == 0u) return false;
-    const uint32_t n = __hip_atomic_load(&g_simd_live[sel - 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t n = lds_load_nodma(&g_simd_live[sel - 1u]);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)n) <= 1u;
 }
 __device__ __forceinline__ uint32_t bal_word() {
@@ -280,6 +296,8 @@ __device__ __forceinline__ uint32_t bal_word() {
 }
 __device__ __forceinline__ void balance_prio(uint32_t blk) {
     const uint32_t me = bal_word();
+    // (atomics, not lds_load_nodma: the inline-asm form spilled the fused
+    // kernel; the compiler's vmcnt wait stays on this overlapped-cycles path)
     __hip_atomic_store(g_bal_prog + me, blk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const uint32_t* row = g_bal_prog + (me & ~15u);
     uint32_t ahead = 0;

@@ -5,7 +5,7 @@
 # alternating; (3) a traced run of each (queue ends, list-group ends).
 set -uo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/r04l3; mkdir -p $O
+O=gpurun_out/r04l7; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -k "fused or full_size or pipeline" -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 export MIRSHA_AB=1
