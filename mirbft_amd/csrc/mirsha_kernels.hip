@@ -284,8 +284,9 @@ __device__ __forceinline__ uint32_t lds_load_nodma(const uint32_t* p) {
 // profiles/r04k: 7,424 vs 5,991 cycles per compression at one wave per SIMD,
 // 5,314 vs 5,607 at four).
 __shared__ uint32_t g_simd_live[4];
+constexpr uint32_t kLoneSeen = 0xFFFFFFFFu;  // hash_tile's lone_sel once the wave has been seen alone
 __device__ __forceinline__ bool simd_alone(uint32_t sel) {  // sel = SIMD + 1 (0: never)
-    if (sel == 0u) return false;
+    if (sel == 0u || sel == kLoneSeen) return sel != 0u;
     const uint32_t n = lds_load_nodma(&g_simd_live[sel - 1u]);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)n) <= 1u;
 }
@@ -724,8 +725,10 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
                 }
                 block_prio(blk);
                 if constexpr (kFused) {
-                    // the SIMD's only live wave: latency round form (g_simd_live)
-                    if (simd_alone(lone_sel)) {  // wave-uniform
+                    // the SIMD's only live wave: latency round form (g_simd_live;
+                    // the count only falls, so once alone the wave stops reading it)
+                    if (lone_sel != 0u && simd_alone(lone_sel)) lone_sel = kLoneSeen;
+                    if (lone_sel == kLoneSeen) {  // wave-uniform
                         if (lone_tr != nullptr) {  // traced runs: the first lone block (bits 53..62, flag 63)
                             if (lane == 0u) *lone_tr |= 1ull << 63 | (unsigned long long)min(blk, 1023u) << 53;
                             lone_tr = nullptr;
