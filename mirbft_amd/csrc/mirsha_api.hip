@@ -1291,7 +1291,8 @@ int fused_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint64_
     if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_LONE_FORM")) a.lone_form = atoi(e) != 0 ? 1u : 0u;
     // The last queue's tile waves stage two blocks ahead (FusedArgs::deep_last).
     // A/B: MIRSHA_FUSED_DEEP_LAST=0.
-    a.deep_last = 1u;
+    a.deep_last = overlap ? 0u : 1u;  // (overlapped launches: no lone stretch, and one DMA in flight keeps
+                                      // the progress ranks' LDS wait free, hash_tile)
     if (const char* e = mirsha::ab_getenv("MIRSHA_FUSED_DEEP_LAST")) a.deep_last = atoi(e) != 0 ? 1u : 0u;
     a.seg_nb = p->d_seg_nb.as<uint32_t>();
     a.seg_state = p->d_seg_state.as<uint32_t>();

@@ -700,6 +700,12 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
                     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
                 else
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // Fused tile waves set the block's priority here, right after the
+                // wait for this block's DMA: kPrioBalance's LDS words are plain
+                // LDS ops, before which hipcc waits for every in-flight LDS-DMA
+                // (lds_load_nodma); here that wait is already paid (one block
+                // in flight; the deep staging is off in overlapped launches).
+                if constexpr (kFused) block_prio(blk);
                 uint32_t w[16];
                 const uint4* tb = tile_of(blk);
 #pragma unroll
@@ -723,7 +729,7 @@ __device__ __forceinline__ uint32_t hash_tile(const uint8_t* __restrict__ arena,
                             pad_words(soff + 16u * (uint32_t)k, L, blk + 1u == nb, (uint32_t)k, &w[4 * k]);
                     }
                 }
-                block_prio(blk);
+                if constexpr (!kFused) block_prio(blk);
                 if constexpr (kFused) {
                     // the SIMD's only live wave: latency round form (g_simd_live;
                     // the count only falls, so once alone the wave stops reading it)
