@@ -10,6 +10,8 @@
 //   4  mode 3 + the per-block s_setprio and LDS live-count read of the fused loop
 //   5  mode 3 with the throughput round form (issue yields)
 //   6  mode 3 + the per-block s_setprio only;  7  mode 3 + the LDS live-count read only
+//   8  mode 3 in the fused loop's shape: both round forms in the loop, chosen by a
+//      cached flag, each under a per-lane block-count test
 // Prints SIMD cycles per block at the clock s_memtime / s_memrealtime reports.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -I mirbft_amd/csrc -o tools/lone_probe tools/lone_probe.hip
@@ -73,6 +75,9 @@ __global__ __launch_bounds__(256, 1) void lone(const uint8_t* __restrict__ arena
         __builtin_amdgcn_s_waitcnt(0);
     }
     const uint32_t n = (uint32_t)nblk;
+    uint32_t lone_sel = wv + 1u;                     // (mode 8)
+    const bool live_flag = g_live[wv] <= 1u;          // (mode 8: alone from the start)
+    const uint32_t nb_lane = n + (lane & 1u);         // (mode 8: a per-lane block count, >= n)
     if constexpr (MODE >= 2) {
         issue(0u);
         if (deep && 1u < n) issue(1u);
@@ -110,10 +115,18 @@ __global__ __launch_bounds__(256, 1) void lone(const uint8_t* __restrict__ arena
             const uint32_t lv = __hip_atomic_load(&g_live[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             alone = (uint32_t)__builtin_amdgcn_readfirstlane((int)lv) <= 1u;
         }
-        if (MODE == 5 || !alone)
+        if constexpr (MODE == 8) {  // the fused loop's shape: both round forms, a per-lane block count
+            if (lone_sel != 0u && live_flag) lone_sel = 0xFFFFFFFFu;
+            if (lone_sel == 0xFFFFFFFFu) {
+                if (b < nb_lane) compress_asm_lat(st, w);
+            } else if (b < nb_lane) {
+                compress_asm(st, w);
+            }
+        } else if (MODE == 5 || !alone) {
             compress_asm(st, w);
-        else
+        } else {
             compress_asm_lat(st, w);
+        }
     }
     const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     uint32_t acc = 0;
@@ -179,6 +192,7 @@ int main(int argc, char** argv) {
         run<5>(d_arena, (uint32_t)bytes, d_out, d_clk, cus, nblk);
         run<6>(d_arena, (uint32_t)bytes, d_out, d_clk, cus, nblk);
         run<7>(d_arena, (uint32_t)bytes, d_out, d_clk, cus, nblk);
+        run<8>(d_arena, (uint32_t)bytes, d_out, d_clk, cus, nblk);
     }
     CHECK(hipFree(d_arena));
     CHECK(hipFree(d_out));
