@@ -786,6 +786,46 @@ def test_fused_placement_fallback(engine, monkeypatch, placement):
     plan.close()
 
 
+@pytest.mark.parametrize("lone,deep", [("1", "1"), ("0", "1"), ("1", "0"), ("0", "0")])
+def test_fused_lone_stretch_forms(engine, monkeypatch, lone, deep):
+    """The last queue's lone stretch (hash_tile in the fused launch): the
+    latency round form once the wave is alone on its SIMD (g_simd_live) and
+    the two-blocks-ahead staging, each on and off (MIRSHA_FUSED_LONE_FORM,
+    MIRSHA_FUSED_DEEP_LAST): config-3-shaped tiles plus split tiles, three
+    runs and an overlapped cycle, bit-exact vs the oracle every way."""
+    torch = _torch()
+    monkeypatch.setenv("MIRSHA_AB", "1")
+    monkeypatch.setenv("MIRSHA_FUSED_LONE_FORM", lone)
+    monkeypatch.setenv("MIRSHA_FUSED_DEEP_LAST", deep)
+    n, stride = 64 * 4100 - 3, 16 + 4096
+    seed = synth.SEED_BASE + 90
+    arena = oracle_py.gen_requests(seed, 0, n, 4096)
+    off = np.arange(n, dtype=np.uint64) * stride
+    lens = np.full(n, stride, dtype=np.uint32)
+    idx, first = sharding.batch_lists(n, 500)
+    plan = engine.pipeline(n, idx, first, lens, mode="fused")
+    assert plan.mode_name == "fused" and plan.split_tiles()[0] > 0
+    want_req = oracle_py.hash_requests(arena, off, lens, threads=8)
+    want_lst = oracle_py.batch_digests(want_req, idx, first)
+    for req, lst in _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=3):
+        assert np.array_equal(req, want_req)
+        assert np.array_equal(lst, want_lst)
+    d_arena = torch.from_numpy(arena).cuda()
+    d_off = torch.from_numpy(off.view(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.view(np.int32)).cuda()
+    d_req = [torch.zeros((n, 32), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d_lst = torch.zeros((first.size - 1, 32), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    args = (d_arena.data_ptr(), arena.size, d_off.data_ptr(), d_len.data_ptr())
+    engine.pipeline_overlap_device(plan, *args, d_req[0].data_ptr(), 0, d_lst.data_ptr())
+    engine.pipeline_overlap_device(plan, *args, d_req[1].data_ptr(), d_req[0].data_ptr(), d_lst.data_ptr())
+    engine.sync()
+    plan.status()
+    assert np.array_equal(d_req[1].cpu().numpy(), want_req)
+    assert np.array_equal(d_lst.cpu().numpy(), want_lst)
+    plan.close()
+
+
 def test_fused_watchdog_fails_closed(engine, monkeypatch):
     """A fused run whose readiness waits expire (test-only zero watchdog,
     MIRSHA_TEST_FUSED_WATCHDOG=0) fails closed: the plan's status is
