@@ -20,9 +20,13 @@ host API call (dedup + pack + H2D + kernel + D2H), so this config is
 PCIe-inclusive by nature.  A synthetic stand-in: the testengine run that
 BASELINE config 4 names needs Go, which this image lacks.
 
-Multi-GPU: one process per GPU (torchrun); every rank hashes its own request
-range (weak scaling), no collective in the data path; the barrier and
-max-over-ranks timing use torch.distributed.
+Multi-GPU: one process per GPU; every rank hashes its own request range (weak
+scaling), no collective in the data path; the barrier and max-over-ranks
+timing use torch.distributed.  `--gpus N` starts the N ranks itself (child
+processes, before anything touches a GPU: launch_ranks) unless a launcher
+(torchrun) already set WORLD_SIZE, in which case --gpus must equal it.  The
+reference scales its hashing with cores the same way, one worker per core
+(processor.go:401-408, HashWorkers = runtime.NumCPU()).
 
 Prints ONE JSON line (rank 0).
 """
@@ -31,18 +35,35 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from mirbft_amd import Engine, MultiEngine, sharding  # noqa: E402
-from mirbft_amd.engine import KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS, KERNEL_OVERLAP  # noqa: E402
+# Product imports happen in _import_product(), after the launcher decision:
+# the launching parent never loads the engine or touches a device.
+torch = None
+Engine = MultiEngine = sharding = None
+KERNEL_CHAIN = KERNEL_FUSED = KERNEL_LISTS = KERNEL_MSGS = KERNEL_OVERLAP = None
+
+
+def _import_product():
+    global torch, Engine, MultiEngine, sharding
+    global KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS, KERNEL_MSGS, KERNEL_OVERLAP
+    import torch as _torch
+
+    from mirbft_amd import Engine as _E, MultiEngine as _M, sharding as _s
+    from mirbft_amd import engine as _eng
+
+    torch, Engine, MultiEngine, sharding = _torch, _E, _M, _s
+    KERNEL_CHAIN, KERNEL_FUSED, KERNEL_LISTS = _eng.KERNEL_CHAIN, _eng.KERNEL_FUSED, _eng.KERNEL_LISTS
+    KERNEL_MSGS, KERNEL_OVERLAP = _eng.KERNEL_MSGS, _eng.KERNEL_OVERLAP
 
 SEED_BASE = 0x6D69726266740000
 # Algorithmic work unit: one 64-byte SHA-256 compression = 1384 int32 VALU ops
@@ -68,14 +89,18 @@ def blocks(L):
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one process per GPU); without a launcher's WORLD_SIZE, bench.py starts them itself")
+    p.add_argument("--launch-check", action="store_true",
+                   help="launcher plumbing only (CPU tests): ranks rendezvous over gloo, barrier, gather their "
+                        "request ranges, rank 0 prints the line with value null; no device, no hashing")
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=100,
                    help="untimed steps; MI355X needs ~20+ ms of sustained load to reach its working clock")
     p.add_argument("--config", type=int, default=2, choices=[1] + sorted(CONFIGS),
                    help="BASELINE config (1 = small-cycle latency of the host API)")
     p.add_argument("--requests", type=int, default=0, help="requests per GPU (0 = the config's)")
-    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6, 10, 11, 12, 13, 14, 15],
+    p.add_argument("--variant", type=int, default=0, choices=[0, 1, 4, 5, 6, 10],
                    help="0 = LDS-staged loader (latency forms for small launches), 1 = direct per-lane loads, "
                         "4 = low-occupancy kernel, 5 = LDS kernel only, 6 = pair kernel")
     p.add_argument("--windows", action="store_true",
@@ -891,17 +916,116 @@ def config3_leg(a, eng, dev):
     return out
 
 
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a):
+    """`--gpus N` without a launcher: start N rank processes of this script
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1),
+    forward rank 0's stdout, and return non-zero if any rank fails (the others
+    are then stopped by PID).  The parent only counts devices
+    (torch.cuda.device_count(), which does not initialise the GPU) and never
+    execs: the ranks are children."""
+    n = a.gpus
+    rehearsal = bool(os.environ.get("MIRSHA_BENCH_DEVICE"))
+    if not rehearsal and not a.launch_check:
+        import torch as _torch
+
+        vis = _torch.cuda.device_count()
+        if vis < n:
+            print(f"bench.py: --gpus {n} but {vis} device(s) visible (set MIRSHA_BENCH_DEVICE=<d> to rehearse "
+                  f"{n} ranks on one device)", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+
+    def forward(stream):
+        for line in stream:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    fw = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+    fw.start()
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.remove(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                print(f"bench.py: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+                for q in live:
+                    procs[q].terminate()
+                deadline = time.time() + 30
+                for q in live:
+                    try:
+                        procs[q].wait(timeout=max(deadline - time.time(), 0.1))
+                    except subprocess.TimeoutExpired:
+                        procs[q].kill()
+        time.sleep(0.05)
+    fw.join(timeout=10)
+    return rc
+
+
+def launch_check(a, world, rank):
+    """--launch-check: the N>1 plumbing without a device (CPU tests): gloo
+    rendezvous, barrier, each rank's request range (BatchWorkload's weak
+    scaling: rank r hashes [r n, (r + 1) n)), gather, rank 0's line."""
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    n = a.requests or CONFIGS[a.config if a.config in CONFIGS else 2][1]
+    info = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
+            "first_request": rank * n, "requests": n}
+    per_rank = [info]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, info)
+    if rank == 0:
+        print(json.dumps({"metric": "SHA-256 digests/s (request + batch digests), Actions.Hash stream",
+                          "value": None, "unit": "digests/s", "n_gpus": world, "steps": a.steps,
+                          "warmup": a.warmup, "launch_check": True, "per_rank": per_rank,
+                          "note": "launcher plumbing only: no device, no hashing"}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the launcher's WORLD_SIZE is {world}")
+    if a.launch_check:
+        launch_check(a, world, rank)
+        return
+    _import_product()
     # Rehearsal knobs for the N>1 path on a one-GPU box (never set by the
     # driver): every rank on device MIRSHA_BENCH_DEVICE, barriers and
     # reductions over gloo instead of RCCL.
     if os.environ.get("MIRSHA_BENCH_DEVICE"):
         local = int(os.environ["MIRSHA_BENCH_DEVICE"])
-    backend = os.environ.get("MIRSHA_BENCH_DIST_BACKEND", "nccl")
+    backend = os.environ.get("MIRSHA_BENCH_DIST_BACKEND",
+                             "gloo" if os.environ.get("MIRSHA_BENCH_DEVICE") else "nccl")
     dist = None
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -1076,7 +1200,7 @@ def main():
                 "workload": f"config{a.config}: {wl.desc}",
                 **wl.config_fields(),
                 "parallelism": f"request-range shards x{world}, no collective",
-                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair", 10: "cu", 11: "cu_noyield", 12: "cu_prefetch", 13: "cu_dma_pipe", 14: "cu_diag_noloads", 15: "cu_diag_noprio"}[a.variant],
+                "kernel_variant": {0: "lds", 1: "direct", 4: "lowocc", 5: "lds_only", 6: "pair", 10: "cu"}[a.variant],
             },
             "gb_per_s_hashed": gbps,
             "roofline": {

@@ -86,11 +86,11 @@ void* mirsha_ctx_stream(mirsha_ctx* ctx);
  * 5 = the LDS kernel at any size, 6 = the pair kernel at any size,
  * 10 = the CU-block kernel at any size (groups beyond 4 per SIMD run in
  *     later workgroups, one CU at a time).
- * A/B forms of the CU-block kernel, accepted only with MIRSHA_AB=1 in the
- * environment (else EINVAL): 11 = register-prefetching block loop with
- * no-yield rounds, 12 = register-prefetching block loop (round 3's form),
- * 13 = LDS-DMA with the next block read back mid-block.
- * All are bit-exact.  2, 3, 7, 8 (round-1 A/B forms) are retired: EINVAL. */
+ * All of these are bit-exact.  Anything else is EINVAL: 2, 3, 7, 8 (round-1
+ * A/B forms) are retired, and 11-15 (retired and diagnostic forms of the
+ * CU-block kernel, one of which skips its loads) exist only in the tools A/B
+ * build (tools/ab_build.sh lib), never in this library, whatever the
+ * environment says. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
 /* Per-kernel device-time accounting with HIP events on the launch stream.

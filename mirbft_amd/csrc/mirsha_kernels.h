@@ -21,25 +21,34 @@ enum : int {
     kVariantLdsOnly = 5,
     kVariantPair = 6,
     kVariantCu = 10,      // CU-block form (one workgroup per CU, LDS-DMA loads one block ahead; <= 4 tiles per SIMD)
-    // A/B forms of the CU-block kernel, accepted only with MIRSHA_AB=1:
+    // Forms of the CU-block kernel compiled ONLY into the tools A/B library
+    // (tools/ab_build.sh lib, -DMIRSHA_AB_FORMS; never the product):
     kVariantCuNoYield = 11,  // register-prefetching block loop, no-yield rounds
     kVariantCuPrefetch = 12, // register-prefetching block loop (round 3's product form)
     kVariantCuDmaPipe = 13,  // LDS-DMA, the next block's words read back mid-block
-    // diagnostics (MIRSHA_AB=1; 14's digests are not valid): the product form
-    kVariantCuDiagNoLoads = 14,  // without its block loads
-    kVariantCuDiagNoPrio = 15,   // without its per-block issue priorities
+    kVariantCuDiagNoLoads = 14,  // diagnostic: without its block loads (its digests are NOT valid)
+    kVariantCuDiagNoPrio = 15,   // diagnostic: without its per-block issue priorities
 };
 const char* ab_getenv(const char* name);
+inline bool variant_is_ab_form(int v) {
+#ifdef MIRSHA_AB_FORMS
+    return v >= kVariantCuNoYield && v <= kVariantCuDiagNoPrio;
+#else
+    (void)v;
+    return false;  // the product library accepts bit-exact forms only
+#endif
+}
 inline bool variant_valid(int v) {
-    if (v >= kVariantCuNoYield && v <= kVariantCuDiagNoPrio) return ab_getenv("MIRSHA_AB") != nullptr;
     return v == kVariantLds || v == kVariantDirect || v == kVariantLowOcc || v == kVariantLdsOnly || v == kVariantPair ||
-           v == kVariantCu;
+           v == kVariantCu || variant_is_ab_form(v);
 }
 constexpr uint32_t kCuMaxWavesPerSimd = 4;
 uint32_t cu_count();
 // Schedule A/B and diagnostic knobs are read from the environment only when
-// MIRSHA_AB=1 is set too (never in production; none changes a digest).
-const char* ab_getenv(const char* name);
+// MIRSHA_AB=1 is set too (never in production).  Every knob the product
+// library reads keeps the digests bit-exact (tests/test_gpu_parity.py runs
+// them); the one form that does not (variant 14) exists only in the tools
+// A/B library.
 constexpr uint32_t kLowOccTiles = 1024;   // 256 CUs x 4 SIMDs
 // Small launches take a latency form: at most pair_max_groups() 64-message
 // groups (default kPairMaxGroups: <= 2 pairs per CU, every wave alone on a

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <cstdio>
 
 #include "mirsha_kernels.h"
 #include "sha256_device.h"
@@ -1785,7 +1786,7 @@ __global__ __launch_bounds__(kPacedMaxThreads) void sha256_fused_paced_kernel(Fu
     // every (simd, slot) of the block is held by exactly one wave -- some then
     // share a physical SIMD, which is slower but complete.  (Round 3 failed
     // such a run closed; plans probe the placement at creation and fall back
-    // to the sequential plan when it is not cyclic, mirsha_api.hip.)
+    // to the sequential plan when it is not cyclic, mirsha_plan.hip.)
     // FusedArgs::test_placement (MIRSHA_AB=1 MIRSHA_TEST_PLACEMENT=remap)
     // makes every wave read SIMD 0, so the remap runs on real hardware.
     __shared__ uint32_t simd_waves[4];
@@ -2148,6 +2149,12 @@ const char* ab_getenv(const char* name) {
 
 uint32_t pair_max_groups() {
     static const uint32_t v = [] {
+        // Round 4 moved MIRSHA_PAIR behind MIRSHA_AB=1: say so once
+        // to a caller still setting it alone, rather than ignoring it silently.
+        if ((getenv("MIRSHA_PAIR") || getenv("MIRSHA_PAIR_MAX_GROUPS")) && !ab_getenv("MIRSHA_PAIR_MAX_GROUPS") &&
+            !ab_getenv("MIRSHA_PAIR"))
+            fprintf(stderr, "mirsha: MIRSHA_PAIR / MIRSHA_PAIR_MAX_GROUPS are A/B knobs, read only with MIRSHA_AB=1; "
+                            "ignored\n");
         const char* e = ab_getenv("MIRSHA_PAIR");
         if (e && e[0] == '0') return 0u;
         const char* m = ab_getenv("MIRSHA_PAIR_MAX_GROUPS");
@@ -2204,12 +2211,14 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
-    if (variant == kVariantCu || variant == kVariantCuNoYield || variant == kVariantCuPrefetch || variant == kVariantCuDmaPipe || variant == kVariantCuDiagNoLoads ||
-        variant == kVariantCuDiagNoPrio ||
+    if (variant == kVariantCu || variant_is_ab_form(variant) ||
         (variant == kVariantLds && tiles <= kCuMaxWavesPerSimd * 4u * cu_count())) {
         // k waves per SIMD, one workgroup of 4k waves per CU
         const uint32_t k = (tiles + 4u * cu_count() - 1u) / (4u * cu_count());
         const uint32_t wg_waves = 4u * std::min(k, kCuMaxWavesPerSimd);
+        const uint32_t cgrid = (tiles + wg_waves - 1u) / wg_waves;
+#ifdef MIRSHA_AB_FORMS
+        // tools/ab_build.sh lib: the retired and diagnostic forms (11-15)
         const int form = variant == kVariantCuNoYield ? 1 : variant == kVariantCuPrefetch ? 2
                          : variant == kVariantCuDmaPipe ? 3 : variant == kVariantCuDiagNoLoads ? 4
                          : variant == kVariantCuDiagNoPrio ? 5 : 0;
@@ -2218,7 +2227,6 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
                               (const void*)sha256_msgs_cu_kernel<4>, (const void*)sha256_msgs_cu_kernel<5>};
         const int slots[6] = {0, 1, 2, 5, 6, 7};  // dyn_lds_attr forms (3: fused, 4: placement probe)
         if (hipError_t e = dyn_lds_attr(fns[form], slots[form], kCuLds)) return e;
-        const uint32_t cgrid = (tiles + wg_waves - 1u) / wg_waves;
         if (form == 4)
             sha256_msgs_cu_kernel<4><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         else if (form == 5)
@@ -2230,7 +2238,11 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         else if (form == 3)
             sha256_msgs_cu_kernel<3><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
         else
+#endif
+        {
+            if (hipError_t e = dyn_lds_attr((const void*)sha256_msgs_cu_kernel<0>, 0, kCuLds)) return e;
             sha256_msgs_cu_kernel<0><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+        }
         return hipGetLastError();
     }
     if (variant == kVariantDirect)

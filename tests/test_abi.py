@@ -90,3 +90,15 @@ def test_no_gpu_multi_is_an_error_not_a_fallback():
         MultiEngine([0])
     with pytest.raises(MirshaError):
         MultiEngine([])
+
+
+def test_product_library_has_no_ab_kernel_forms():
+    """The retired / diagnostic CU-block forms (variants 11-15, one of which
+    skips its loads) are compiled only into the tools A/B build
+    (tools/ab_build.sh lib, -DMIRSHA_AB_FORMS): the product library holds the
+    product instantiation of sha256_msgs_cu_kernel and no other."""
+    import subprocess
+
+    out = subprocess.run(["nm", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    forms = sorted(set(re.findall(r"sha256_msgs_cu_kernelILi(\d+)E", out)))
+    assert forms == ["0"], forms

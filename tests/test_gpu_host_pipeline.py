@@ -1,4 +1,4 @@
-"""Pipelined synchronous host calls (run_pipelined in mirsha_api.hip): calls
+"""Pipelined synchronous host calls (run_pipelined in mirsha_staging.hip): calls
 whose packed arena exceeds one 32 MiB staging chunk go over PCIe chunk by
 chunk, each chunk's messages hashed as soon as it lands and their digests
 returned while later chunks are still in flight.  Every digest must still be

@@ -23,8 +23,9 @@ pytestmark = pytest.mark.gpu
 EMPTY = "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
 
 
-# A/B kernel forms (accepted by the library only with MIRSHA_AB=1) join the
-# parametrisation when MIRSHA_TEST_AB_VARIANTS lists them, e.g. "12".
+# A/B kernel forms of the tools build (tools/ab_build.sh lib, loaded through
+# MIRSHA_AB_LIB with MIRSHA_AB=1) join the parametrisation when
+# MIRSHA_TEST_AB_VARIANTS lists them, e.g. "12".  The product library rejects them.
 _AB_VARIANTS = [int(v) for v in os.environ.get("MIRSHA_TEST_AB_VARIANTS", "").split(",") if v.strip()]
 
 
@@ -943,6 +944,21 @@ def _contiguous(seed, n, bs, listed, max_len):
     arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
     idx, first = sharding.batch_lists(listed, bs)
     return arena, off, lens, idx, first
+
+
+@pytest.mark.parametrize("variant", [11, 12, 13, 14, 15])
+def test_ab_forms_not_in_product_library(engine, variant, monkeypatch):
+    """Variants 11-15 (retired and diagnostic CU-block forms; 14 skips its
+    loads and writes wrong digests) live only in the tools A/B build: the
+    product library refuses them even with MIRSHA_AB=1."""
+    if os.environ.get("MIRSHA_AB_LIB"):
+        pytest.skip("an A/B build is loaded")
+    monkeypatch.setenv("MIRSHA_AB", "1")
+    with pytest.raises(MirshaError) as e:
+        engine.set_variant(variant)
+    assert e.value.code == _lib.MIRSHA_EINVAL
+    assert _hex(engine.hash_messages([b"abc"])) == [
+        "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"]
 
 
 @pytest.mark.parametrize("variant", [2, 3, 7, 8, 9, -1])
