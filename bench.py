@@ -412,22 +412,30 @@ class BatchWorkload:
     def cgo_path(self):
         """The Go binding's HashBatch end to end, slices -> digests
         (tests/c/cgo_path.c, a separate process with no Python: request
-        Data as 3 heap slices each, packed into the mirsha_host_alloc arena
-        by one or by 16 workers, then mirsha_hash_batch; and the
-        library-packed mirsha_hash_slices).  Config 2 at full size."""
+        Data as 3 heap slices each; a persistent 15-worker pool stands in for
+        the goroutines).  Config 2 at full size.  Legs: 'parallel' =
+        INTEGRATION.md's HashBatch (32 MiB chunks packed into the pinned arena
+        while the calling thread submits the previous one, mirsha_submit_batch), 'onecall' =
+        round 4's (pack all, then one mirsha_hash_batch), 'serial' = one
+        goroutine packs, 'lib' = mirsha_hash_slices, 'multi' = the chunked
+        form over every device (mirsha_submit_arena_multi)."""
         exe = os.path.join(ROOT, "tests", "c", "build", "cgo_path")
         if not os.path.exists(exe):
             return {"note": f"{exe} not built (__graft_entry__.build())"}
-        r = subprocess.run([exe, str(self.n), str(self.data_len), "16", "5"], capture_output=True, text=True,
+        # 15 packing workers + the submitting thread = the GPU box's 16-CPU share
+        r = subprocess.run([exe, str(self.n), str(self.data_len), "15", "7", "32"], capture_output=True, text=True,
                            timeout=300)
         if r.returncode != 0:
             return {"error": r.stderr[-500:]}
         out = json.loads(r.stdout.splitlines()[-1])
         out.pop("sample", None)
-        out["note"] = ("INTEGRATION.md GPUHasher.HashBatch made from C: 'serial' = one goroutine packs, "
-                       "'parallel' = 16 goroutines (GOMAXPROCS chunks), 'lib' = mirsha_hash_slices on C slice "
-                       "arrays (library packing overlapped with the DMA); median of 5 calls, digests into pageable "
-                       "memory, PCIe included")
+        out["note"] = ("INTEGRATION.md GPUHasher.HashBatch made from C: 'parallel' = the chunked form (15 workers "
+                       "pack chunk k+1 while the caller submits chunk k, mirsha_submit_batch: DMA / kernel / D2H on "
+                       "three streams; digests DMA'd into a pinned buffer, copied to the Go-owned result by the "
+                       "workers), 'onecall' = pack "
+                       "everything then one mirsha_hash_batch, 'serial' = one goroutine packs, 'lib' = "
+                       "mirsha_hash_slices on C slice arrays, 'multi' = the chunked form over every visible device "
+                       "(device 0 twice on one GPU); median of 7 calls, PCIe included, every leg's digests equal")
         return out
 
     def cpu_baseline(self, seconds):

@@ -177,6 +177,26 @@ int mirsha_submit_slices(mirsha_ctx* ctx, const uint8_t* const* slice_ptr,
                          uint8_t* digests_out, int flags, uint64_t* ticket_out);
 int mirsha_wait(mirsha_ctx* ctx, uint64_t ticket);
 int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
+/* The same ring over a caller arena (mirsha_hash_batch's arguments): request
+ * i = arena[off[i] .. off[i]+len[i]).  For the Go binding's chunked HashBatch
+ * (replaces processor.go:133-143 for one Ready() cycle): the
+ * caller packs chunk k+1 of the cycle into a page-locked arena
+ * (mirsha_host_alloc) while chunk k, already submitted, is DMA'd, hashed and
+ * its digests copied back.
+ *   off / len are read before the call returns (Go memory is fine there).
+ *   A page-locked arena is DMA'd straight from the caller's memory: its bytes
+ *     [min off, max off+len) must not change until the ticket retires.  A
+ *     pageable arena is copied into the context's staging before the call
+ *     returns.
+ *   digests_out: C memory, valid until the ticket retires (as
+ *     mirsha_submit_slices).  Page-locked (mirsha_host_alloc) digests_out
+ *     receives the digests by DMA with no host copy.
+ *   At most MIRSHA_MAX_DEVICE_ARENA_BYTES of request bytes per submission
+ *   (else MIRSHA_ERANGE; submit the cycle in chunks).  Shares the ring (4 in
+ *   flight) and the tickets of mirsha_submit_slices: mirsha_wait / mirsha_poll. */
+int mirsha_submit_batch(mirsha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
+                        const uint64_t* off, const uint32_t* len, uint32_t n,
+                        uint8_t* digests_out, uint64_t* ticket_out);
 
 /* Host-side phases (milliseconds) of the context's last host-API call.
  * Slice submissions (mirsha_submit_slices / mirsha_hash_slices_dedup):
@@ -405,7 +425,8 @@ int mirsha_multi_devices(const mirsha_multi* m);
 /* Context of device index k (0 <= k < ndev) for per-device settings and
  * diagnostics (mirsha_ctx_set_variant, timing); owned by m. */
 mirsha_ctx* mirsha_multi_ctx(mirsha_multi* m, int k);
-/* Request-range cut of the last call: first_out[k] = first request of device
+/* Request-range cut of the last call (every entry point cuts at the request
+ * boundary nearest to k/ndev of the bytes): first_out[k] = first request of device
  * index k, first_out[ndev] = n.  Returns ndev + 1 (entries written: min(cap, ndev + 1)). */
 int mirsha_multi_last_cut(const mirsha_multi* m, uint32_t* first_out, int cap);
 int mirsha_hash_slices_multi(mirsha_multi* m, const uint8_t* const* slice_ptr,
@@ -425,6 +446,14 @@ int mirsha_multi_host_alloc(mirsha_multi* m, uint64_t bytes, void** out);
 int mirsha_submit_slices_multi(mirsha_multi* m, const uint8_t* const* slice_ptr,
                                const uint64_t* slice_len, const uint32_t* slice_first, uint32_t n,
                                uint8_t* digests_out, int flags, uint64_t* ticket_out);
+/* mirsha_submit_batch over several devices: the requests cut into contiguous
+ * ranges of equal bytes (as mirsha_hash_arena_multi), each range submitted to
+ * its device's ring, DMA'd straight from a page-locked arena
+ * (mirsha_multi_host_alloc) over that device's own link.  Tickets, wait and
+ * poll as mirsha_submit_slices_multi. */
+int mirsha_submit_arena_multi(mirsha_multi* m, const uint8_t* arena, uint64_t arena_len,
+                              const uint64_t* off, const uint32_t* len, uint32_t n,
+                              uint8_t* digests_out, uint64_t* ticket_out);
 int mirsha_wait_multi(mirsha_multi* m, uint64_t ticket);
 int mirsha_poll_multi(mirsha_multi* m, uint64_t ticket, int* done);
 /* mirsha_ctx_host_profile of device index k's last call (its range only). */

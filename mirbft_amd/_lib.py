@@ -58,6 +58,7 @@ SIGNATURES = {
     "mirsha_submit_slices": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_void_p, c_int, _u64p]),
     "mirsha_wait": (c_int, [c_void_p, c_uint64]),
     "mirsha_poll": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
+    "mirsha_submit_batch": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p, _u64p]),
     "mirsha_hash_requests_then_batches": (
         c_int,
         [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p, c_uint32, c_void_p, c_void_p],
@@ -116,6 +117,10 @@ SIGNATURES = {
     ),
     "mirsha_hash_arena_multi": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p]),
     "mirsha_multi_host_alloc": (c_int, [c_void_p, c_uint64, POINTER(c_void_p)]),
+    "mirsha_submit_arena_multi": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, c_void_p, _u64p],
+    ),
     "mirsha_wait_multi": (c_int, [c_void_p, c_uint64]),
     "mirsha_poll_multi": (c_int, [c_void_p, c_uint64, POINTER(c_int)]),
     "mirsha_multi_host_profile": (c_int, [c_void_p, c_int, POINTER(c_double), c_int]),

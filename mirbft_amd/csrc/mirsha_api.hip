@@ -132,6 +132,8 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->xin) (void)hipStreamSynchronize(c->xin);
+    if (c->xout) (void)hipStreamSynchronize(c->xout);
     for (auto& t : c->timers) {
         for (auto& pr : t.pending) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
         for (auto e : t.pool) (void)hipEventDestroy(e);
@@ -152,6 +154,8 @@ void mirsha_ctx_destroy(mirsha_ctx* c) {
     for (auto& sl : c->slots) {
         sl.stage.release(); sl.dig.release(); sl.dev.release(); sl.stage2.release(); sl.dev2.release();
         if (sl.done) (void)hipEventDestroy(sl.done);
+        if (sl.ev_in) (void)hipEventDestroy(sl.ev_in);
+        if (sl.ev_kern) (void)hipEventDestroy(sl.ev_kern);
     }
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;

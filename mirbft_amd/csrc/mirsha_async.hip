@@ -12,8 +12,10 @@ int async_complete(mirsha_ctx* c, AsyncSlot& sl) {
     const auto t_done = Clock::now();
     sl.prof[MIRSHA_PROF_DEVICE] = std::chrono::duration<double, std::milli>(t_done - sl.t_queued).count();
     const uint8_t* d = sl.dig.as<uint8_t>();
-    if (sl.rank.empty()) {
-        memcpy(sl.user_out, d, 32ull * sl.n);
+    if (sl.direct) {
+        // mirsha_submit_batch into page-locked digests_out: already there
+    } else if (sl.rank.empty()) {
+        if (sl.n) memcpy(sl.user_out, d, 32ull * sl.n);
     } else {
         for (uint32_t i = 0; i < sl.n; i++) memcpy(sl.user_out + 32ull * i, d + 32ull * sl.rank[i], 32);
     }
@@ -66,6 +68,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     if (sl.busy)
         if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
     sl.rank.clear();
+    sl.direct = false;
     HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
     if (!sl.done) HIP_TRY(c, hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
     ph[MIRSHA_PROF_PLAN] = ms_since(t0);
@@ -176,6 +179,173 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     return MIRSHA_OK;
 }
 
+
+// mirsha_submit_batch: n requests of a caller arena (request i =
+// arena[off[i], off[i] + len[i])), one slot of the ring.  The off / len
+// arrays are read before the call returns.  A dense range [lo, hi) of a
+// page-locked arena is DMA'd straight from it (no host copy: the caller must
+// leave those bytes alone until the ticket retires); a pageable or sparse one
+// is copied into the slot's pinned staging first (packed back to back when
+// sparse), so the caller may reuse it at once.  Digests land in a page-locked
+// digests_out by DMA, else in the slot's pinned rows, copied out when the
+// ticket retires.  The Go binding's chunked HashBatch packs
+// chunk k + 1 of a Ready() cycle while chunk k's DMA, kernel and D2H run.
+int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                       const uint32_t* len, uint32_t n, uint8_t* out, uint64_t* ticket_out) {
+    auto t0 = Clock::now();
+    double ph[MIRSHA_PROF_PHASES] = {};
+    // One pass over the n entries: bounds, the span [lo, hi), total bytes,
+    // block-count range; off / len copied into the metadata staging on the
+    // way (rebased below).  A chunk of the Go binding's HashBatch is ~60k
+    // requests and its goroutines are packing the NEXT chunk meanwhile, so
+    // the pass stays on the calling thread up to 2^18 requests (a pass per
+    // concern, with pool dispatches, cost ~0.2 ms per chunk).
+    struct Part {
+        uint64_t lo = UINT64_MAX, hi = 0, tot = 0;
+        uint32_t bmin = UINT32_MAX, bmax = 0, bad = UINT32_MAX;
+    };
+    const int T = n < (1u << 18) ? 1
+                                 : (int)std::min<uint32_t>((uint32_t)mirsha::host::max_threads(), n / (1u << 16));
+    std::vector<Part> parts(T);
+    const uint32_t step = n ? (n + (uint32_t)T - 1) / (uint32_t)T : 1;
+    // staging: [request bytes (unless DMA'd from the caller) | off u64 | len u32 | order u32];
+    // the metadata block first goes at its offset for a copied arena, which needs
+    // the span; written at offset 0 of a separate region, then placed below.
+    if (int rc = use_device(c)) return rc;
+    AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
+    if (sl.busy)
+        if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
+    const uint64_t meta_bytes = align8(16ull * n);
+    HIP_TRY(c, sl.stage2.ensure(std::max<uint64_t>(meta_bytes, 8)));  // metadata block of arena submissions
+    uint8_t* mb = sl.stage2.as<uint8_t>();
+    uint64_t* soff = reinterpret_cast<uint64_t*>(mb);
+    uint32_t* slen = reinterpret_cast<uint32_t*>(mb + 8ull * n);
+    uint32_t* sord = slen + n;
+    mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
+        Part& q = parts[a / step];
+        for (uint32_t i = a; i < b; i++) {
+            const uint64_t o = off[i];
+            const uint32_t L = len[i];
+            if (L > MIRSHA_MAX_MESSAGE_BYTES || o > arena_len || L > arena_len - o) {
+                q.bad = i;
+                return;
+            }
+            soff[i] = o;
+            slen[i] = L;
+            q.lo = std::min(q.lo, o);
+            q.hi = std::max(q.hi, o + L);
+            q.tot += L;
+            const uint32_t k = host_blocks(L);
+            q.bmin = std::min(q.bmin, k);
+            q.bmax = std::max(q.bmax, k);
+        }
+    });
+    Part all;
+    for (const Part& q : parts) {
+        all.bad = std::min(all.bad, q.bad);
+        all.lo = std::min(all.lo, q.lo);
+        all.hi = std::max(all.hi, q.hi);
+        all.tot += q.tot;
+        all.bmin = std::min(all.bmin, q.bmin);
+        all.bmax = std::max(all.bmax, q.bmax);
+    }
+    if (all.bad != UINT32_MAX) {
+        const uint32_t i = all.bad;
+        if (len[i] > MIRSHA_MAX_MESSAGE_BYTES)
+            return fail(c, MIRSHA_ERANGE, "message %u is %u bytes (max %u)", i, len[i], MIRSHA_MAX_MESSAGE_BYTES);
+        return fail(c, MIRSHA_EINVAL, "message %u [%llu,+%u) outside arena of %llu bytes", i,
+                    (unsigned long long)off[i], len[i], (unsigned long long)arena_len);
+    }
+    const uint64_t lo = n ? all.lo : 0, hi = n ? all.hi : 0, total = all.tot;
+    const uint64_t span = hi - lo;
+    const bool dense = span <= 2 * total + 4096;
+    const uint64_t bytes = dense ? span : total;
+    if (bytes + kArenaSlack > MIRSHA_MAX_DEVICE_ARENA_BYTES)
+        return fail(c, MIRSHA_ERANGE, "submission of %llu bytes exceeds one device arena (%u); split it",
+                    (unsigned long long)bytes, MIRSHA_MAX_DEVICE_ARENA_BYTES);
+    if (dense) {
+        if (lo)
+            mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
+                for (uint32_t i = a; i < b; i++) soff[i] -= lo;
+            });
+    } else {  // packed back to back: off = exclusive scan of len
+        uint64_t p = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            soff[i] = p;
+            p += len[i];
+        }
+    }
+    const bool identity = n == 0 || all.bmin == all.bmax || bucket_order(slen, n, sord);
+    ph[MIRSHA_PROF_VALIDATE] = ms_since(t0);
+    t0 = Clock::now();
+    sl.rank.clear();
+    for (hipEvent_t* e : {&sl.done, &sl.ev_in, &sl.ev_kern})
+        if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    // Three streams, as the pipelined synchronous calls: request bytes and
+    // metadata in on xin, the kernel on the context stream, digests out on
+    // xout.  Submission k+1's DMA runs behind submission k's DMA, not behind
+    // its kernel and D2H (PCIe is full duplex).
+    if (!c->xin) HIP_TRY(c, hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
+    if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
+    const bool from_caller = dense && n && host_pinned(arena + lo);
+    sl.direct = host_pinned(out);
+    if (!sl.direct) HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
+    // device: [request bytes + slack | off u64 | len u32 | order u32 | digests]
+    const uint64_t o_len = 8ull * n, o_ord = o_len + 4ull * n, o_end = meta_bytes;
+    const uint64_t d_meta = align8(bytes + kArenaSlack), d_dig = d_meta + o_end;
+    if (!from_caller) HIP_TRY(c, sl.stage.ensure(std::max<uint64_t>(bytes, 8)));
+    HIP_TRY(c, sl.dev.ensure(d_dig + 32ull * n));
+    uint8_t* st = sl.stage.as<uint8_t>();
+    ph[MIRSHA_PROF_PLAN] = ms_since(t0);
+    t0 = Clock::now();
+    uint8_t* dv = sl.dev.as<uint8_t>();
+    if (from_caller) {
+        HIP_TRY(c, hipMemcpyAsync(dv, arena + lo, bytes, hipMemcpyHostToDevice, c->xin));
+    } else if (dense) {
+        mirsha::host::pack_range(arena + lo, nullptr, nullptr, nullptr, 0, nullptr, 0, bytes, st,
+                                 mirsha::host::threads_for(bytes, 1u << 20));
+    } else {
+        std::vector<const uint8_t*> sp(n);
+        std::vector<uint64_t> sz(n);
+        std::vector<uint32_t> sf(n + 1);
+        for (uint32_t i = 0; i < n; i++) {
+            sp[i] = arena + off[i];
+            sz[i] = len[i];
+            sf[i] = i;
+        }
+        sf[n] = n;
+        mirsha::host::pack(sp.data(), sz.data(), sf.data(), nullptr, n, soff, st, mirsha::host::threads_for(bytes, n));
+    }
+    if (n) {
+        if (!from_caller && bytes) HIP_TRY(c, hipMemcpyAsync(dv, st, bytes, hipMemcpyHostToDevice, c->xin));
+        HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, o_end, hipMemcpyHostToDevice, c->xin));
+        HIP_TRY(c, hipEventRecord(sl.ev_in, c->xin));
+        HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.ev_in, 0));
+        if (int rc = timed_launch(c, 0, [&] {
+                return mirsha::launch_msgs(dv, bytes, reinterpret_cast<const uint64_t*>(dv + d_meta),
+                                           reinterpret_cast<const uint32_t*>(dv + d_meta + o_len),
+                                           identity ? nullptr : reinterpret_cast<const uint32_t*>(dv + d_meta + o_ord),
+                                           n, dv + d_dig, c->variant, c->stream);
+            }))
+            return rc;
+        HIP_TRY(c, hipEventRecord(sl.ev_kern, c->stream));
+        HIP_TRY(c, hipStreamWaitEvent(c->xout, sl.ev_kern, 0));
+        HIP_TRY(c, hipMemcpyAsync(sl.direct ? out : sl.dig.as<uint8_t>(), dv + d_dig, 32ull * n, hipMemcpyDeviceToHost,
+                                  c->xout));
+    }
+    HIP_TRY(c, hipEventRecord(sl.done, c->xout));
+    sl.t_queued = Clock::now();
+    ph[MIRSHA_PROF_PACK] = ms_since(t0);
+    sl.busy = true;
+    sl.user_out = out;
+    sl.n = n;
+    sl.m = n;
+    sl.ticket = c->next_ticket++;
+    for (int k = 0; k < MIRSHA_PROF_PHASES; k++) sl.prof[k] = ph[k];
+    *ticket_out = sl.ticket;
+    return MIRSHA_OK;
+}
+
 }  // namespace mirsha_api
 
 extern "C" {
@@ -195,6 +365,13 @@ int mirsha_submit_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const u
                          const uint32_t* slice_first, uint32_t n, uint8_t* out, int flags, uint64_t* ticket_out) {
     if (!c || !ticket_out) return MIRSHA_EINVAL;
     return async_submit(c, slice_ptr, slice_len, slice_first, n, out, flags, ticket_out, nullptr);
+}
+
+int mirsha_submit_batch(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                        const uint32_t* len, uint32_t n, uint8_t* digests_out, uint64_t* ticket_out) {
+    if (!c || !ticket_out) return MIRSHA_EINVAL;
+    if (n && (!off || !len || !digests_out || (!arena && arena_len))) return fail(c, MIRSHA_EINVAL, "NULL argument");
+    return async_submit_arena(c, arena, arena_len, off, len, n, digests_out, ticket_out);
 }
 
 int mirsha_wait(mirsha_ctx* c, uint64_t ticket) {

@@ -108,9 +108,11 @@ struct AsyncSlot {
     PinnedBuf stage2;  // a dedup submission's second launch (representatives
     DevBuf dev2;       // found after the first), queued behind the first
     hipEvent_t done = nullptr;
+    hipEvent_t ev_in = nullptr, ev_kern = nullptr;  // arena submissions: H2D landed, kernel done
     uint64_t ticket = 0;
     bool busy = false;
     uint8_t* user_out = nullptr;
+    bool direct = false;  // digests DMA'd straight into a page-locked user_out (nothing to copy at retire)
     uint32_t n = 0, m = 0;
     std::vector<uint32_t> rank;  // request -> row of `dig` (empty: identity)
     double prof[MIRSHA_PROF_PHASES] = {};  // this submission's host phases (published when it completes)

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <thread>
 #include <unordered_map>
@@ -180,10 +181,13 @@ class Pool {
 Pool& pool() {
     static Pool* p = new Pool(max_threads() - 1);
     if (t_pool_slot <= 0) return *p;
+    // Keyed by (slot, threads): a later mirsha_multi with a different share
+    // of the host threads gets a pool of its own size.  Pools are
+    // kept for the process (their workers park on a condition variable).
     static std::mutex mu;
-    static Pool* extra[kMaxPools] = {};
+    static std::map<std::pair<int, int>, Pool*> extra;
     std::lock_guard<std::mutex> g(mu);
-    Pool*& q = extra[t_pool_slot];
+    Pool*& q = extra[{t_pool_slot, t_pool_threads}];
     if (!q) q = new Pool(std::max(t_pool_threads, 1) - 1);
     return *q;
 }

@@ -173,6 +173,35 @@ int multi_fail(mirsha_multi* m, int code, const char* msg) {
     return code;
 }
 
+// m->cut from inclusive prefix sums of the request bytes (empty requests
+// counting 1): the request boundary nearest to k/nd of the bytes for every
+// k, so each device's share is within half a request of the fair one.  Both
+// the slice and the arena entry points cut this way.
+void cut_nearest(mirsha_multi* m, const std::vector<uint64_t>& sum) {
+    const uint32_t n = (uint32_t)sum.size();
+    const uint64_t total = n ? sum[n - 1] : 0;
+    const int nd = (int)m->ctx.size();
+    m->cut.assign(nd + 1, n);
+    m->cut[0] = 0;
+    for (int k = 1; k < nd; k++) {
+        const uint64_t want = (total * (uint64_t)k + nd / 2) / nd;
+        uint32_t i = (uint32_t)(std::lower_bound(sum.begin(), sum.end(), want) - sum.begin());  // sum[i] >= want
+        if (i < n && (i == 0 ? want : want - sum[i - 1]) * 2 > (sum[i] - (i ? sum[i - 1] : 0))) i++;
+        m->cut[k] = std::max(std::min(i, n), m->cut[k - 1]);
+    }
+}
+
+// Arena form: the same cut over the request lengths.
+void arena_cut(mirsha_multi* m, const uint32_t* len, uint32_t n) {
+    std::vector<uint64_t> sum(n);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        total += std::max<uint32_t>(len[i], 1u);
+        sum[i] = total;
+    }
+    cut_nearest(m, sum);
+}
+
 // Validates the slice lists (as mirsha_hash_slices does) and cuts [0, n) into
 // one contiguous range per device with equal bytes (ranges may be empty).
 int multi_cut(mirsha_multi* m, const uint8_t* const* slice_ptr, const uint64_t* slice_len,
@@ -209,16 +238,7 @@ int multi_cut(mirsha_multi* m, const uint8_t* const* slice_ptr, const uint64_t* 
         total += std::max<uint64_t>(sum[i], 1);
         sum[i] = total;
     }
-    const int nd = (int)m->ctx.size();
-    m->cut.assign(nd + 1, n);
-    m->cut[0] = 0;
-    for (int k = 1; k < nd; k++) {
-        // the request boundary nearest to k/nd of the bytes
-        const uint64_t want = (total * (uint64_t)k + nd / 2) / nd;
-        uint32_t i = (uint32_t)(std::lower_bound(sum.begin(), sum.end(), want) - sum.begin());  // sum[i] >= want
-        if (i < n && (i == 0 ? want : want - sum[i - 1]) * 2 > (sum[i] - (i ? sum[i - 1] : 0))) i++;
-        m->cut[k] = std::max(std::min(i, n), m->cut[k - 1]);
-    }
+    cut_nearest(m, sum);
     return MIRSHA_OK;
 }
 
@@ -314,18 +334,7 @@ int mirsha_hash_arena_multi(mirsha_multi* m, const uint8_t* arena, uint64_t aren
     m->err.clear();
     if (n == 0) return MIRSHA_OK;
     if (!off || !len || !digests_out || (!arena && arena_len)) return multi_fail(m, MIRSHA_EINVAL, "NULL argument");
-    // equal-bytes cut over the request lengths (empty requests count 1)
-    const int nd = (int)m->ctx.size();
-    uint64_t total = 0;
-    for (uint32_t i = 0; i < n; i++) total += std::max<uint32_t>(len[i], 1u);
-    m->cut.assign(nd + 1, n);
-    m->cut[0] = 0;
-    uint64_t acc = 0;
-    int d = 1;
-    for (uint32_t i = 0; i < n && d < nd; i++) {
-        acc += std::max<uint32_t>(len[i], 1u);
-        while (d < nd && acc * (uint64_t)nd >= total * (uint64_t)d) m->cut[d++] = i + 1;
-    }
+    arena_cut(m, len, n);  // equal bytes, nearest request boundary (as multi_cut)
     return multi_run(m, [&](int k) -> int {
         const uint32_t a = m->cut[k], b = m->cut[k + 1];
         if (a >= b) return MIRSHA_OK;
@@ -377,6 +386,37 @@ int mirsha_submit_slices_multi(mirsha_multi* m, const uint8_t* const* slice_ptr,
         // a device refused its range: retire the ranges the others queued
         // before returning, so no digest lands in digests_out after the
         // failed call (the caller may free it)
+        const std::string err = m->err;
+        for (size_t k = 0; k < dt.size(); k++)
+            if (dt[k]) (void)mirsha_wait(m->ctx[k], dt[k]);
+        m->err = err;
+        return rc;
+    }
+    m->dev_tickets[(t - 1) % kMultiAsyncSlots] = dt;
+    m->next_ticket++;
+    *ticket_out = t;
+    return MIRSHA_OK;
+}
+
+int mirsha_submit_arena_multi(mirsha_multi* m, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                              const uint32_t* len, uint32_t n, uint8_t* digests_out, uint64_t* ticket_out) {
+    if (!m || !ticket_out) return MIRSHA_EINVAL;
+    m->err.clear();
+    if (n && (!off || !len || !digests_out || (!arena && arena_len))) return multi_fail(m, MIRSHA_EINVAL, "NULL argument");
+    const uint64_t t = m->next_ticket;
+    if (t > (uint64_t)kMultiAsyncSlots && m->done_ticket < t - kMultiAsyncSlots)
+        if (int rc = mirsha_wait_multi(m, t - kMultiAsyncSlots)) return rc;
+    arena_cut(m, len, n);
+    const int nd = (int)m->ctx.size();
+    std::vector<uint64_t> dt(nd, 0);
+    const int rc = multi_run(m, [&](int k) -> int {
+        const uint32_t a = m->cut[k], b = m->cut[k + 1];
+        if (a >= b) return MIRSHA_OK;
+        return mirsha_submit_batch(m->ctx[k], arena, arena_len, off + a, len + a, b - a, digests_out + 32ull * a,
+                                   &dt[k]);
+    });
+    if (rc) {
+        // as mirsha_submit_slices_multi: nothing lands after a failed call
         const std::string err = m->err;
         for (size_t k = 0; k < dt.size(); k++)
             if (dt[k]) (void)mirsha_wait(m->ctx[k], dt[k]);

@@ -274,6 +274,26 @@ class Engine:
         self._retire(t.value - ASYNC_SLOTS)
         return Ticket(t.value, out)
 
+    def submit_batch(self, arena, off, length, out=None) -> "Ticket":
+        """Asynchronous arena submission (mirsha_submit_batch, the Go binding's
+        chunked HashBatch): request i = arena[off[i]:off[i]+len[i]].  A
+        page-locked arena (host_empty) is DMA'd from in place and must not
+        change until the ticket is waited for; a page-locked ``out`` receives
+        the digests by DMA."""
+        a = _as_u8(arena)
+        o = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(length, dtype=np.uint32)
+        if o.shape != ln.shape:
+            raise ValueError("off and len differ in length")
+        n = int(o.size)
+        out = _out_rows(out, n)
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.mirsha_submit_batch(self.ctx, _ptr(a), a.size, _ptr(o), _ptr(ln), n, _ptr(out),
+                                                  ctypes.byref(t)))
+        self._outstanding[t.value] = (out, a)  # the arena too: it may be read until the ticket retires
+        self._retire(t.value - ASYNC_SLOTS)
+        return Ticket(t.value, out)
+
     def _retire(self, upto: int) -> None:
         for k in [k for k in self._outstanding if k <= upto]:
             del self._outstanding[k]
@@ -594,6 +614,23 @@ class MultiEngine:
                                                          _ptr(out), _lib.MIRSHA_SUBMIT_DEDUP if dedup else 0,
                                                          ctypes.byref(t)))
         self._outstanding[t.value] = out
+        for k in [k for k in self._outstanding if k <= t.value - ASYNC_SLOTS]:
+            del self._outstanding[k]
+        return Ticket(t.value, out)
+
+    def submit_arena(self, arena, off, length, out=None) -> "Ticket":
+        """mirsha_submit_arena_multi: Engine.submit_batch over every device."""
+        a = _as_u8(arena)
+        o = np.ascontiguousarray(off, dtype=np.uint64)
+        ln = np.ascontiguousarray(length, dtype=np.uint32)
+        if o.shape != ln.shape:
+            raise ValueError("off and len differ in length")
+        n = int(o.size)
+        out = _out_rows(out, n)
+        t = ctypes.c_uint64(0)
+        self._check(self._lib.mirsha_submit_arena_multi(self.handle, _ptr(a), a.size, _ptr(o), _ptr(ln), n, _ptr(out),
+                                                        ctypes.byref(t)))
+        self._outstanding[t.value] = (out, a)
         for k in [k for k in self._outstanding if k <= t.value - ASYNC_SLOTS]:
             del self._outstanding[k]
         return Ticket(t.value, out)

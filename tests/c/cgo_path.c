@@ -5,21 +5,32 @@
  *
  * Input: n client requests as the state machine hands them to the Processor
  * (state_machine.go:313-317: Data = [LE64(client), LE64(reqNo), payload]),
- * every slice its own heap allocation, as Go's [][]byte slices are.  Legs,
- * each the median of `reps` calls after one warm-up:
- *   serial    HashBatch as round 2 wrote it: one goroutine packs every slice
- *             into the mirsha_host_alloc arena, then mirsha_hash_batch;
- *   parallel  the same, the copy split over `threads` workers in contiguous
- *             request chunks (GOMAXPROCS goroutines), offsets computed first;
+ * every slice its own heap allocation, as Go's [][]byte slices are.  A
+ * persistent pool of `threads` workers stands in for GOMAXPROCS goroutines
+ * (a goroutine start costs ~1 us; a pthread_create per chunk would not).
+ * Legs, each the median of `reps` calls after one warm-up:
+ *   serial    round 2's HashBatch: one goroutine packs every slice into the
+ *             mirsha_host_alloc arena, then one mirsha_hash_batch;
+ *   parallel  INTEGRATION.md's HashBatch: offsets first, then the cycle in
+ *             chunks of ~chunk_mib MiB: the workers pack chunk k into the
+ *             pinned arena (and copy the digests of chunks already back into
+ *             the Go-owned result buffer), then mirsha_submit_batch queues its
+ *             DMA + kernel + D2H (into a pinned digest buffer) and returns, so
+ *             chunk k's transfer overlaps chunk k+1's packing; mirsha_wait on
+ *             the last ticket, the remaining digests copied by the workers;
+ *   onecall   round 4's HashBatch: the workers pack the whole cycle, then one
+ *             mirsha_hash_batch (no overlap of packing and DMA);
  *   lib       mirsha_hash_slices on C arrays of the slice pointers: the
- *             library's own 16-thread packing into its pinned ring,
- *             overlapped with the DMA (what a binding could use if the slices
- *             were C memory; Go's cgo rules forbid passing Go pointers stored
- *             in C memory, so the Go binding copies first).
- * Prints ONE JSON line; "sample" carries the first 4 digests of each leg for
- * tests/test_c_abi.py to compare with the oracle.  Exit 0 = ok.
+ *             library's own packing into its pinned ring, overlapped with the
+ *             DMA (what a binding could use if the slices were C memory; Go's
+ *             cgo rules forbid passing Go pointers stored in C memory);
+ *   multi     GPUHasherMulti.HashBatch: `parallel` over every visible device
+ *             (device 0 twice on a one-GPU box) with mirsha_submit_arena_multi.
+ * Prints ONE JSON line; "sample" carries the first 4 digests for
+ * tests/test_c_abi.py to compare with the oracle; every leg's digests are
+ * compared with the serial leg's.  Exit 0 = ok.
  *
- * Usage: cgo_path [n] [data_len] [threads] [reps]
+ * Usage: cgo_path [n] [data_len] [threads] [reps] [chunk_mib]
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
@@ -32,12 +43,14 @@
 #include "mirsha.h"
 
 static mirsha_ctx* ctx = NULL;
+static mirsha_multi* multi = NULL;
 
 #define CHECK(call)                                                                                     \
     do {                                                                                                \
         int rc_ = (call);                                                                               \
         if (rc_ != MIRSHA_OK) {                                                                         \
-            fprintf(stderr, "%s failed: %d: %s\n", #call, rc_, ctx ? mirsha_last_error(ctx) : "");     \
+            fprintf(stderr, "%s failed: %d: %s\n", #call, rc_,                                         \
+                    multi ? mirsha_multi_last_error(multi) : ctx ? mirsha_last_error(ctx) : "");        \
             exit(2);                                                                                    \
         }                                                                                               \
     } while (0)
@@ -61,31 +74,127 @@ typedef struct {
     uint64_t len[3];
 } Request;
 
-/* The binding's per-call buffers (Go: make([]uint64, n) etc.). */
+/* ---- worker pool (GOMAXPROCS goroutines + sync.WaitGroup) ---- */
+typedef void (*PartFn)(void* arg, int part, int parts);
+typedef struct Pool Pool;
+typedef struct {
+    Pool* pool;
+    int idx;
+} PoolSeat;
+struct Pool {
+    pthread_t th[64];
+    PoolSeat seat[64];
+    int n;
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    uint64_t gen;
+    int pending, quit;
+    PartFn fn;
+    void* arg;
+};
+
+static void* pool_worker(void* a) {
+    PoolSeat* s = (PoolSeat*)a;
+    Pool* p = s->pool;
+    uint64_t seen = 0;
+    for (;;) {
+        pthread_mutex_lock(&p->mu);
+        while (p->gen == seen && !p->quit) pthread_cond_wait(&p->go, &p->mu);
+        if (p->quit) {
+            pthread_mutex_unlock(&p->mu);
+            return NULL;
+        }
+        seen = p->gen;
+        PartFn fn = p->fn;
+        void* arg = p->arg;
+        pthread_mutex_unlock(&p->mu);
+        fn(arg, s->idx, p->n);
+        pthread_mutex_lock(&p->mu);
+        if (--p->pending == 0) pthread_cond_signal(&p->done);
+        pthread_mutex_unlock(&p->mu);
+    }
+}
+
+static void pool_init(Pool* p, int n) {
+    memset(p, 0, sizeof(*p));
+    p->n = n;
+    pthread_mutex_init(&p->mu, NULL);
+    pthread_cond_init(&p->go, NULL);
+    pthread_cond_init(&p->done, NULL);
+    for (int i = 0; i < n; i++) {
+        p->seat[i] = (PoolSeat){p, i};
+        if (pthread_create(&p->th[i], NULL, pool_worker, &p->seat[i]) != 0) exit(4);
+    }
+}
+
+/* fn(arg, part, n) on every worker (go func() ... for each part); pool_wait
+ * is the WaitGroup.Wait. */
+static void pool_start(Pool* p, PartFn fn, void* arg) {
+    pthread_mutex_lock(&p->mu);
+    p->fn = fn;
+    p->arg = arg;
+    p->pending = p->n;
+    p->gen++;
+    pthread_cond_broadcast(&p->go);
+    pthread_mutex_unlock(&p->mu);
+}
+
+static void pool_wait(Pool* p) {
+    pthread_mutex_lock(&p->mu);
+    while (p->pending) pthread_cond_wait(&p->done, &p->mu);
+    pthread_mutex_unlock(&p->mu);
+}
+
+static void pool_run(Pool* p, PartFn fn, void* arg) {
+    pool_start(p, fn, arg);
+    pool_wait(p);
+}
+
+static void pool_stop(Pool* p) {
+    pthread_mutex_lock(&p->mu);
+    p->quit = 1;
+    pthread_cond_broadcast(&p->go);
+    pthread_mutex_unlock(&p->mu);
+    for (int i = 0; i < p->n; i++) pthread_join(p->th[i], NULL);
+}
+
+static void part_range(uint32_t lo, uint32_t hi, int part, int parts, uint32_t* a, uint32_t* b) {
+    const uint32_t n = hi - lo, step = (n + (uint32_t)parts - 1) / (uint32_t)parts;
+    const uint32_t x = (uint32_t)part * step;
+    *a = lo + (x < n ? x : n);
+    *b = lo + (x + step < n ? x + step : n);
+}
+
+/* One pool job: pack requests [lo, hi) into the arena at off[i] (h.Write of
+ * every Data slice, processor.go:135-137), and copy digest rows [dlo, dhi)
+ * from the pinned digest buffer into the caller's. */
 typedef struct {
     const Request* reqs;
     uint8_t* arena;
     const uint64_t* off;
     uint32_t lo, hi;
-} PackJob;
+    const uint8_t* dsrc;
+    uint8_t* ddst;
+    uint32_t dlo, dhi;
+} ChunkJob;
 
-static void* pack_range(void* arg) {
-    const PackJob* j = (const PackJob*)arg;
-    for (uint32_t i = j->lo; i < j->hi; i++) {
+static void chunk_part(void* arg, int part, int parts) {
+    const ChunkJob* j = (const ChunkJob*)arg;
+    uint32_t a, b;
+    part_range(j->lo, j->hi, part, parts, &a, &b);
+    for (uint32_t i = a; i < b; i++) {
         uint8_t* dst = j->arena + j->off[i];
         for (int s = 0; s < 3; s++) {
             memcpy(dst, j->reqs[i].ptr[s], j->reqs[i].len[s]);
             dst += j->reqs[i].len[s];
         }
     }
-    return NULL;
+    part_range(j->dlo, j->dhi, part, parts, &a, &b);
+    if (b > a) memcpy(j->ddst + 32ull * a, j->dsrc + 32ull * a, 32ull * (b - a));
 }
 
-/* HashBatch: offsets and lengths, the copy into the pinned arena (threads
- * workers), one mirsha_hash_batch.  Returns {pack ms, call ms}. */
-static void hash_batch(const Request* reqs, uint32_t n, uint8_t* arena, uint64_t* off, uint32_t* lens, uint8_t* dig,
-                       int threads, double* pack_ms, double* call_ms) {
-    const double t0 = now_ms();
+/* offsets and lengths of the cycle (Go: off[i], lens[i], serial); returns the total */
+static uint64_t offsets(const Request* reqs, uint32_t n, uint64_t* off, uint32_t* lens) {
     uint64_t p = 0;
     for (uint32_t i = 0; i < n; i++) {
         off[i] = p;
@@ -93,25 +202,155 @@ static void hash_batch(const Request* reqs, uint32_t n, uint8_t* arena, uint64_t
         lens[i] = (uint32_t)l;
         p += l;
     }
-    if (threads <= 1) {
-        PackJob j = {reqs, arena, off, 0, n};
-        pack_range(&j);
-    } else {
-        pthread_t th[64];
-        PackJob jobs[64];
-        const uint32_t step = (n + (uint32_t)threads - 1) / (uint32_t)threads;
-        for (int t = 0; t < threads; t++) {
-            const uint32_t lo = (uint32_t)t * step < n ? (uint32_t)t * step : n;
-            const uint32_t hi = lo + step < n ? lo + step : n;
-            jobs[t] = (PackJob){reqs, arena, off, lo, hi};
-            if (pthread_create(&th[t], NULL, pack_range, &jobs[t]) != 0) exit(4);
-        }
-        for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    return p;
+}
+
+/* offsets by the pool: a two-pass scan (lengths and per-part sums, then the
+ * offsets of each part from the prefix of the sums) */
+typedef struct {
+    const Request* reqs;
+    uint32_t n;
+    uint64_t* off;
+    uint32_t* lens;
+    uint64_t part_sum[65];
+} OffJob;
+
+static void off_sum_part(void* arg, int part, int parts) {
+    OffJob* j = (OffJob*)arg;
+    uint32_t a, b;
+    part_range(0, j->n, part, parts, &a, &b);
+    uint64_t s = 0;
+    for (uint32_t i = a; i < b; i++) {
+        const uint64_t l = j->reqs[i].len[0] + j->reqs[i].len[1] + j->reqs[i].len[2];
+        j->lens[i] = (uint32_t)l;
+        s += l;
     }
+    j->part_sum[part + 1] = s;
+}
+
+static void off_write_part(void* arg, int part, int parts) {
+    OffJob* j = (OffJob*)arg;
+    uint32_t a, b;
+    part_range(0, j->n, part, parts, &a, &b);
+    uint64_t p = j->part_sum[part];
+    for (uint32_t i = a; i < b; i++) {
+        j->off[i] = p;
+        p += j->lens[i];
+    }
+}
+
+static uint64_t offsets_parallel(const Request* reqs, uint32_t n, uint64_t* off, uint32_t* lens, Pool* pool) {
+    static OffJob j;
+    j.reqs = reqs;
+    j.n = n;
+    j.off = off;
+    j.lens = lens;
+    j.part_sum[0] = 0;
+    pool_run(pool, off_sum_part, &j);
+    for (int k = 0; k < pool->n; k++) j.part_sum[k + 1] += j.part_sum[k];
+    pool_run(pool, off_write_part, &j);
+    return j.part_sum[pool->n];
+}
+
+/* Round 2 / round 4 HashBatch: pack everything (1 or `pool` workers), one
+ * mirsha_hash_batch.  {pack ms, call ms}. */
+static void hash_batch_onecall(const Request* reqs, uint32_t n, uint8_t* arena, uint64_t* off, uint32_t* lens,
+                               uint8_t* dig, Pool* pool, double* pack_ms, double* call_ms) {
+    const double t0 = now_ms();
+    const uint64_t total = offsets(reqs, n, off, lens);
+    ChunkJob j = {reqs, arena, off, 0, n, NULL, NULL, 0, 0};
+    if (pool)
+        pool_run(pool, chunk_part, &j);
+    else
+        chunk_part(&j, 0, 1);
     const double t1 = now_ms();
-    CHECK(mirsha_hash_batch(ctx, arena, p, off, lens, n, dig));
+    CHECK(mirsha_hash_batch(ctx, arena, total, off, lens, n, dig));
     *pack_ms = t1 - t0;
     *call_ms = now_ms() - t1;
+}
+
+/* INTEGRATION.md's HashBatch (single device, or a mirsha_multi when m != NULL):
+ * offsets by the workers, then chunk k+1 packed by the workers WHILE the
+ * caller submits chunk k (mirsha_submit_batch returns once its DMA, kernel
+ * and D2H are queued), so neither the submission's host work nor the DMA
+ * waits for packing.  {pack ms = until the last submission returned, call ms
+ * = wait + the last digests}.  *chunks_out = submissions. */
+#define MAX_CHUNKS 4096
+/* host phases of the last chunked call (ms): offsets, waiting for the packing
+ * workers, submits (overlapping the packing), final wait, final copy */
+static double ph_off, ph_pack, ph_submit, ph_wait, ph_copy;
+static void submit_chunk(mirsha_multi* m, const uint8_t* arena, uint64_t total, const uint64_t* off,
+                         const uint32_t* lens, uint32_t lo, uint32_t hi, uint8_t* dig_pinned, uint64_t* ticket) {
+    if (m)
+        CHECK(mirsha_submit_arena_multi(m, arena, total, off + lo, lens + lo, hi - lo, dig_pinned + 32ull * lo, ticket));
+    else
+        CHECK(mirsha_submit_batch(ctx, arena, total, off + lo, lens + lo, hi - lo, dig_pinned + 32ull * lo, ticket));
+}
+
+static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, uint64_t* off, uint32_t* lens,
+                               uint8_t* dig_pinned, uint8_t* dig, Pool* pool, uint64_t chunk_bytes, mirsha_multi* m,
+                               double* pack_ms, double* call_ms, int* chunks_out) {
+    static uint64_t ticket[MAX_CHUNKS];
+    static uint32_t cfirst[MAX_CHUNKS + 1];
+    const double t0 = now_ms();
+    const uint64_t total = offsets_parallel(reqs, n, off, lens, pool);
+    ph_off = now_ms() - t0;
+    ph_pack = ph_submit = 0.0;
+    /* chunk boundaries: requests [lo, hi) until the chunk's bytes reach chunk_bytes */
+    int nk = 0;
+    for (uint32_t lo = 0; lo < n;) {
+        uint32_t hi = lo + 1;
+        while (hi < n && off[hi] - off[lo] < chunk_bytes) hi++;
+        if (nk == MAX_CHUNKS) exit(6);
+        cfirst[nk++] = lo;
+        lo = hi;
+    }
+    cfirst[nk] = n;
+    int copied = 0; /* chunks whose digests are in dig */
+    ChunkJob job;
+    for (int k = 0; k <= nk; k++) {
+        /* workers: pack chunk k (if any) + the digests of chunks already back */
+        const double tp = now_ms();
+        job = (ChunkJob){reqs, arena, off, k < nk ? cfirst[k] : 0, k < nk ? cfirst[k + 1] : 0, dig_pinned, dig, 0, 0};
+        int upto = copied;
+        while (upto < k - 1) {
+            int done = 0;
+            if (m)
+                CHECK(mirsha_poll_multi(m, ticket[upto], &done));
+            else
+                CHECK(mirsha_poll(ctx, ticket[upto], &done));
+            if (!done) break;
+            upto++;
+        }
+        if (upto > copied) {
+            job.dlo = cfirst[copied];
+            job.dhi = cfirst[upto];
+            copied = upto;
+        }
+        if (k < nk || job.dhi > job.dlo) pool_start(pool, chunk_part, &job);
+        /* caller: submit chunk k-1, packed in the previous round */
+        const double ts = now_ms();
+        if (k > 0) submit_chunk(m, arena, total, off, lens, cfirst[k - 1], cfirst[k], dig_pinned, &ticket[k - 1]);
+        const double tw = now_ms();
+        ph_submit += tw - ts;
+        if (k < nk || job.dhi > job.dlo) pool_wait(pool);
+        ph_pack += (ts - tp) + (now_ms() - tw);
+    }
+    const double t1 = now_ms();
+    if (nk) {
+        if (m)
+            CHECK(mirsha_wait_multi(m, ticket[nk - 1]));
+        else
+            CHECK(mirsha_wait(ctx, ticket[nk - 1]));
+        const double tw = now_ms();
+        ph_wait = tw - t1;
+        job = (ChunkJob){reqs, arena, off, 0, 0, dig_pinned, dig, cfirst[copied], n};
+        pool_run(pool, chunk_part, &job);
+        ph_copy = now_ms() - tw;
+    }
+    *pack_ms = t1 - t0;
+    *call_ms = now_ms() - t1;
+    *chunks_out = nk;
 }
 
 static int cmp_d(const void* a, const void* b) {
@@ -133,14 +372,33 @@ static void hex4(const uint8_t* dig, char* out) {
     }
 }
 
+typedef struct {
+    double pack[64], call[64], tot[64];
+} Leg;
+
+static void leg_put(Leg* l, int r, double a, double b) {
+    if (r < 0) return;
+    l->pack[r] = a;
+    l->call[r] = b;
+    l->tot[r] = a + b;
+}
+
+static void leg_print(const char* name, Leg* l, int reps, uint32_t n, const char* extra) {
+    const double t = median(l->tot, reps);
+    printf("\"%s\": {\"pack_ms\": %.3f, \"call_ms\": %.3f, \"ms\": %.3f, \"digests_per_s\": %.1f%s}", name,
+           median(l->pack, reps), median(l->call, reps), t, n / (t * 1e-3), extra);
+}
+
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? (uint32_t)strtoul(argv[1], NULL, 10) : (1u << 20);
     const uint32_t data_len = argc > 2 ? (uint32_t)strtoul(argv[2], NULL, 10) : 256u;
     int threads = argc > 3 ? atoi(argv[3]) : 16;
     const int reps = argc > 4 ? atoi(argv[4]) : 5;
+    const double chunk_mib = argc > 5 ? atof(argv[5]) : 16.0;
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
-    if (n < 4 || reps < 1 || reps > 64) return 5;
+    if (n < 4 || reps < 1 || reps > 64 || chunk_mib <= 0) return 5;
+    const uint64_t chunk_bytes = (uint64_t)(chunk_mib * 1048576.0);
     int ndev = 0;
     CHECK(mirsha_device_count(&ndev));
     if (ndev < 1) {
@@ -170,21 +428,43 @@ int main(int argc, char** argv) {
         total += 16u + data_len;
     }
     void* ap = NULL;
+    void* dp = NULL;
     CHECK(mirsha_host_alloc(ctx, total + 1, &ap));
+    CHECK(mirsha_host_alloc(ctx, 32ull * n, &dp)); /* the binding's pinned digest buffer */
     uint8_t* arena = ap;
+    uint8_t* dig_pinned = dp;
     uint64_t* off = malloc(8ull * n);
     uint32_t* lens = malloc(4ull * n);
     uint8_t* dig_s = malloc(32ull * n);
     uint8_t* dig_p = malloc(32ull * n);
+    uint8_t* dig_o = malloc(32ull * n);
     uint8_t* dig_l = malloc(32ull * n);
+    uint8_t* dig_m = malloc(32ull * n);
+    Pool pool;
+    pool_init(&pool, threads);
 
-    double pk[64], cl[64], tot[64], pk2[64], cl2[64], tot2[64], lib[64];
+    Leg ser, par, one, lib, mul;
+    char phases[512] = "";
+    int chunks = 0, mchunks = 0;
     for (int r = -1; r < reps; r++) { /* r = -1: warm-up */
         double a, b;
-        hash_batch(reqs, n, arena, off, lens, dig_s, 1, &a, &b);
-        if (r >= 0) pk[r] = a, cl[r] = b, tot[r] = a + b;
-        hash_batch(reqs, n, arena, off, lens, dig_p, threads, &a, &b);
-        if (r >= 0) pk2[r] = a, cl2[r] = b, tot2[r] = a + b;
+        hash_batch_onecall(reqs, n, arena, off, lens, dig_s, NULL, &a, &b);
+        leg_put(&ser, r, a, b);
+        hash_batch_chunked(reqs, n, arena, off, lens, dig_pinned, dig_p, &pool, chunk_bytes, NULL, &a, &b, &chunks);
+        leg_put(&par, r, a, b);
+        if (r == reps - 1) {
+            /* the library's phases of the last chunk's submission (validate, plan, queue) */
+            double lp[MIRSHA_PROF_PHASES] = {0};
+            mirsha_ctx_host_profile(ctx, lp, MIRSHA_PROF_PHASES);
+            snprintf(phases, sizeof phases,
+                     ", \"last_call_phases_ms\": {\"offsets\": %.3f, \"pack\": %.3f, \"submit\": %.3f, "
+                     "\"wait\": %.3f, \"copy\": %.3f}, \"last_submit_ms\": {\"validate\": %.3f, "
+                     "\"plan\": %.3f, \"queue\": %.3f, \"device\": %.3f}",
+                     ph_off, ph_pack, ph_submit, ph_wait, ph_copy, lp[MIRSHA_PROF_VALIDATE], lp[MIRSHA_PROF_PLAN],
+                     lp[MIRSHA_PROF_PACK], lp[MIRSHA_PROF_DEVICE]);
+        }
+        hash_batch_onecall(reqs, n, arena, off, lens, dig_o, &pool, &a, &b);
+        leg_put(&one, r, a, b);
     }
     /* lib: slice pointer arrays in C memory, the library packs */
     const uint8_t** sp = malloc(sizeof(uint8_t*) * 3ull * n);
@@ -201,23 +481,48 @@ int main(int argc, char** argv) {
     for (int r = -1; r < reps; r++) {
         const double t0 = now_ms();
         CHECK(mirsha_hash_slices(ctx, sp, sl, sf, n, dig_l));
-        if (r >= 0) lib[r] = now_ms() - t0;
+        leg_put(&lib, r, 0.0, now_ms() - t0);
     }
-    if (memcmp(dig_s, dig_p, 32ull * n) || memcmp(dig_s, dig_l, 32ull * n)) {
+    /* multi: GPUHasherMulti over every device (device 0 twice on one GPU) */
+    int devs[16], nd = ndev > 1 ? (ndev < 16 ? ndev : 16) : 2;
+    for (int k = 0; k < nd; k++) devs[k] = ndev > 1 ? k : 0;
+    mirsha_host_free(ap);
+    mirsha_host_free(dp);
+    ap = dp = NULL;
+    CHECK(mirsha_multi_create(devs, nd, &multi));
+    CHECK(mirsha_multi_host_alloc(multi, total + 1, &ap));
+    CHECK(mirsha_multi_host_alloc(multi, 32ull * n, &dp));
+    for (int r = -1; r < reps; r++) {
+        double a, b;
+        hash_batch_chunked(reqs, n, ap, off, lens, dp, dig_m, &pool, chunk_bytes, multi, &a, &b, &mchunks);
+        leg_put(&mul, r, a, b);
+    }
+    if (memcmp(dig_s, dig_p, 32ull * n) || memcmp(dig_s, dig_o, 32ull * n) || memcmp(dig_s, dig_l, 32ull * n) ||
+        memcmp(dig_s, dig_m, 32ull * n)) {
         fprintf(stderr, "legs disagree\n");
         return 1;
     }
-    const double m_tot = median(tot, reps), m_tot2 = median(tot2, reps), m_lib = median(lib, reps);
-    char sample[4 * 65 + 8];
+    char sample[4 * 65 + 8], extra[640], mextra[96];
     hex4(dig_s, sample);
-    printf("{\"requests\": %u, \"request_bytes\": %u, \"bytes\": %llu, \"threads\": %d, \"reps\": %d, "
-           "\"serial\": {\"pack_ms\": %.3f, \"call_ms\": %.3f, \"ms\": %.3f, \"digests_per_s\": %.1f}, "
-           "\"parallel\": {\"pack_ms\": %.3f, \"call_ms\": %.3f, \"ms\": %.3f, \"digests_per_s\": %.1f}, "
-           "\"lib\": {\"ms\": %.3f, \"digests_per_s\": %.1f}, \"sample\": \"%s\"}\n",
-           n, 16u + data_len, (unsigned long long)total, threads, reps, median(pk, reps), median(cl, reps), m_tot,
-           n / (m_tot * 1e-3), median(pk2, reps), median(cl2, reps), m_tot2, n / (m_tot2 * 1e-3), m_lib,
-           n / (m_lib * 1e-3), sample);
-    mirsha_host_free(arena);
+    snprintf(extra, sizeof extra, ", \"chunks\": %d, \"chunk_mib\": %.2f%s", chunks, chunk_mib, phases);
+    snprintf(mextra, sizeof mextra, ", \"chunks\": %d, \"devices\": %d", mchunks, nd);
+    printf("{\"requests\": %u, \"request_bytes\": %u, \"bytes\": %llu, \"threads\": %d, \"reps\": %d, ", n,
+           16u + data_len, (unsigned long long)total, threads, reps);
+    leg_print("serial", &ser, reps, n, "");
+    printf(", ");
+    leg_print("parallel", &par, reps, n, extra);
+    printf(", ");
+    leg_print("onecall", &one, reps, n, "");
+    printf(", ");
+    leg_print("lib", &lib, reps, n, "");
+    printf(", ");
+    leg_print("multi", &mul, reps, n, mextra);
+    printf(", \"sample\": \"%s\"}\n", sample);
+    pool_stop(&pool);
+    mirsha_host_free(ap);
+    mirsha_host_free(dp);
+    mirsha_multi_destroy(multi);
+    multi = NULL;
     mirsha_ctx_destroy(ctx);
     return 0;
 }

@@ -6,7 +6,10 @@
  *   mirsha_ctx_create
  *   mirsha_host_alloc (once; the GPUHasher's pinned arena, grown on demand)
  *   per Ready() cycle: pack HashRequest.Data into the arena, mirsha_hash_batch
- *     (GPUHasher.HashBatch; processor.go:129-143)
+ *     (round 4's GPUHasher.HashBatch; processor.go:129-143)
+ *   the chunked HashBatch: chunk k packed into the arena, mirsha_submit_batch
+ *     with a pinned digest buffer (mirsha_host_alloc), mirsha_poll on earlier
+ *     chunks, mirsha_wait on the last
  *   mirsha_submit_slices + mirsha_wait with the slice arrays in C memory
  *     (GPUHasher.SubmitBatch / PendingBatch.Wait; processor.go:447-470)
  *   one-request mirsha_hash_batch calls (gpuHash.Sum, the hash.Hash of
@@ -14,8 +17,10 @@
  *   mirsha_host_free, mirsha_ctx_destroy
  *   GPUHasherMulti (several devices; here device 0 listed twice):
  *     mirsha_multi_create, mirsha_multi_host_alloc (portable pinned arena),
- *     mirsha_hash_arena_multi per cycle, mirsha_submit_slices_multi +
- *     mirsha_wait_multi, mirsha_host_free, mirsha_multi_destroy
+ *     mirsha_hash_arena_multi per cycle, the chunked HashBatch with
+ *     mirsha_submit_arena_multi / mirsha_poll_multi / mirsha_wait_multi,
+ *     mirsha_submit_slices_multi + mirsha_wait_multi, mirsha_host_free,
+ *     mirsha_multi_destroy
  *
  * Requests are the testengine's (testengine/recorder.go:158-174): client c,
  * reqNo r, data = LE64(c) || "-" || LE64(r), hashed as state_machine.go:313-317
@@ -125,6 +130,36 @@ int main(void) {
         done += n;
     }
 
+    /* The chunked HashBatch: the 800 requests packed chunk
+     * by chunk (~3,300 bytes each: 8 chunks, more than the 4-slot ring) into
+     * the arena, each chunk submitted as soon as it is packed; digests DMA'd
+     * into a pinned buffer, polled per chunk, the last chunk waited for. */
+    {
+        uint8_t* a = arena_bytes(33ull * n_total + 1);
+        void* dp = NULL;
+        CHECK(mirsha_host_alloc(ctx, 32ull * n_total, &dp));
+        uint8_t* dig = (uint8_t*)dp;
+        uint64_t* off = malloc(8ull * n_total);
+        uint32_t* len = malloc(4ull * n_total);
+        uint64_t ticket[16];
+        int nk = 0, polled = 0;
+        for (uint32_t lo = 0; lo < n_total; lo += 100, nk++) {
+            for (uint32_t i = lo; i < lo + 100; i++) {
+                off[i] = 33ull * i;
+                len[i] = pack_request(a + off[i], i / 200, i % 200);
+            }
+            CHECK(mirsha_submit_batch(ctx, a, 33ull * n_total, off + lo, len + lo, 100, dig + 32ull * lo, &ticket[nk]));
+            int done = 0;
+            CHECK(mirsha_poll(ctx, ticket[0], &done));
+            polled += done;
+        }
+        CHECK(mirsha_wait(ctx, ticket[nk - 1]));
+        for (uint32_t i = 0; i < n_total; i++) print_hex("chunk", i, dig + 32ull * i);
+        free(off);
+        free(len);
+        mirsha_host_free(dp);
+    }
+
     /* SubmitBatch / Wait: the same 800 requests as one slice each (C arrays,
      * freed after submit returns), dedup on; a second submission of the
      * first 20 in flight at the same time. */
@@ -214,6 +249,21 @@ int main(void) {
         }
         MCHECK(mirsha_hash_arena_multi(m, a, p, off, len, n_total, dig));
         for (uint32_t i = 0; i < n_total; i++) print_hex("multi", i, dig + 32ull * i);
+        /* the chunked HashBatch over the devices: 4 chunks of 200 requests */
+        {
+            void* dp = NULL;
+            MCHECK(mirsha_multi_host_alloc(m, 32ull * n_total, &dp));
+            uint8_t* cd = (uint8_t*)dp;
+            uint64_t ct[4];
+            for (int k = 0; k < 4; k++) {
+                MCHECK(mirsha_submit_arena_multi(m, a, p, off + 200 * k, len + 200 * k, 200, cd + 32ull * 200 * k, &ct[k]));
+                int done = 0;
+                MCHECK(mirsha_poll_multi(m, ct[0], &done));
+            }
+            MCHECK(mirsha_wait_multi(m, ct[3]));
+            for (uint32_t i = 0; i < n_total; i++) print_hex("cmulti", i, cd + 32ull * i);
+            mirsha_host_free(dp);
+        }
         const uint8_t** ptr = malloc(sizeof(uint8_t*) * n_total);
         uint64_t* slen = malloc(8ull * n_total);
         uint32_t* first = malloc(4ull * (n_total + 1));

@@ -43,7 +43,7 @@ def test_cgo_sequence_on_gpu(tmp_path, layouts):
     assert "fips ok" in lines and lines[-1] == "sequence ok"
     want = {200 * e["client"] + e["req_no"]: e["sha256"] for e in layouts["testengine_requests"]}
     assert len(want) == 800
-    for tag in ("req", "async", "multi", "amulti"):
+    for tag in ("req", "chunk", "async", "multi", "cmulti", "amulti"):
         got = {int(i): h for t, i, h in (ln.split() for ln in lines if ln.startswith(tag + " "))}
         assert got == want, tag
 
@@ -56,16 +56,21 @@ def test_cgo_path_compiles_and_links(tmp_path):
 
 @pytest.mark.gpu
 def test_cgo_path_on_gpu(tmp_path):
-    """The binding's HashBatch from C (serial and parallel packing of 3 heap
-    slices per request into the pinned arena, then mirsha_hash_batch; and the
-    library-packed mirsha_hash_slices): the legs agree (checked in the
-    program) and the digests are the oracle's."""
+    """The binding's HashBatch from C: the chunked form INTEGRATION.md now
+    gives (packing of chunk k+1 overlapping chunk k's mirsha_submit_batch),
+    round 4's one-call form, the serial form, the library-packed
+    mirsha_hash_slices and the multi-device twin (mirsha_submit_arena_multi,
+    device 0 twice): every leg agrees with the serial one (checked in the
+    program) and the digests are the oracle's.  A 1 MiB chunk budget gives 26
+    chunks, far more than the 4-slot ring."""
     exe = build(tmp_path, PATH_SRC, "cgo_path")
     n, data_len = 100_003, 256
-    r = subprocess.run([exe, str(n), str(data_len), "8", "2"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, str(n), str(data_len), "8", "2", "1"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     line = json.loads(r.stdout.splitlines()[-1])
     assert line["requests"] == n and line["parallel"]["ms"] > 0
+    per = -(-(1 << 20) // (16 + data_len))  # requests per 1 MiB chunk (the chunk ends at a request boundary)
+    assert line["parallel"]["chunks"] == -(-n // per) == line["multi"]["chunks"] == 26
     arena = oracle_py.gen_requests(0x6D69726266740002, 0, 4, data_len)
     stride = 16 + data_len
     want = oracle_py.hash_requests(arena, np.arange(4, dtype=np.uint64) * stride, np.full(4, stride))

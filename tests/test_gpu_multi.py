@@ -164,3 +164,72 @@ def test_async_multi_error_retires_other_ranges(multi):
     assert e.value.code == _lib.MIRSHA_EINVAL
     t = multi.submit_slices(sl)
     assert np.array_equal(multi.wait(t), _want(reqs))
+
+
+def test_hash_arena_multi_cut_balances_bytes(multi):
+    """The arena form cuts like the slice form: at the request
+    boundary nearest to half the bytes, so the shares differ by at most one
+    request."""
+    lens = np.array([60_000] * 40 + [100] * 24_000, dtype=np.uint32)
+    off = np.zeros(lens.size, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    src = np.random.default_rng(70).integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    got = multi.hash_arena(src, off, lens)
+    assert np.array_equal(got, oracle_py.hash_requests(src, off, lens, threads=8))
+    cut = multi.last_cut()
+    b0, b1 = int(lens[: cut[1]].sum()), int(lens[cut[1]:].sum())
+    assert abs(b0 - b1) <= 60_000, (cut, b0, b1)
+    # the slice form cuts the same input at the same place
+    multi.hash_slices([[src[int(o):int(o) + int(n)].tobytes()] for o, n in zip(off, lens)])
+    assert multi.last_cut() == cut
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_submit_arena_multi_chunked(multi, pinned):
+    """mirsha_submit_arena_multi, the twin of mirsha_submit_batch behind
+    GPUHasherMulti's chunked HashBatch: a cycle in chunks (more than the ring
+    holds), each chunk cut over both contexts, empty requests and messages
+    longer than a chunk budget; bit-exact, origin order."""
+    rng = np.random.default_rng(80 + pinned)
+    n = 40_000
+    lens = rng.integers(0, 900, n).astype(np.uint32)
+    lens[::11] = 0
+    lens[7_000::9_000] = 400_000
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    size = int(off[-1] + lens[-1]) + 1
+    src = rng.integers(0, 256, size, dtype=np.uint8)
+    arena = multi.host_empty(size) if pinned else np.empty(size, dtype=np.uint8)
+    arena[:] = src
+    out = multi.host_empty(32 * n).reshape(n, 32) if pinned else np.empty((n, 32), dtype=np.uint8)
+    bounds = list(range(0, n, 4_000)) + [n]
+    tickets = [multi.submit_arena(arena, off[a:b], lens[a:b], out=out[a:b]) for a, b in zip(bounds, bounds[1:])]
+    assert len(tickets) == 10
+    multi.wait(tickets[-1])
+    assert np.array_equal(out, oracle_py.hash_requests(src, off, lens, threads=8))
+
+
+def test_submit_arena_multi_error_retires_other_ranges(multi):
+    """A failure inside ONE device's range after the other device has queued
+    its own: request 5,500 lies outside the arena, which only the
+    second context's validation sees.  The call fails with EINVAL, the first
+    range's digests are final when it returns, and the next submission is
+    bit-exact."""
+    rng = np.random.default_rng(90)
+    n = 6000
+    lens = rng.integers(1, 500, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    src = rng.integers(0, 256, int(off[-1] + lens[-1]), dtype=np.uint8)
+    want = oracle_py.hash_requests(src, off, lens)
+    bad = off.copy()
+    bad[5500] = src.size
+    out = np.zeros((n, 32), dtype=np.uint8)
+    with pytest.raises(MirshaError) as e:
+        multi.submit_arena(src, bad, lens, out=out)
+    assert e.value.code == _lib.MIRSHA_EINVAL
+    cut = multi.last_cut()
+    assert 0 < cut[1] <= 5500
+    assert np.array_equal(out[: cut[1]], want[: cut[1]])  # the first range, retired before the call returned
+    t = multi.submit_arena(src, off, lens)
+    assert np.array_equal(multi.wait(t), want)
