@@ -303,7 +303,7 @@ def tail_round(j):
         f"v_bitop3_b32 {t1}, {a}, {b}, {c} bitop3:0xe8",
         f"v_add3_u32 {h}, {h}, {t0}, {t1}",
     ]
-    lines = yield_after_complex(lines, COMPLEX, 2)
+    lines = yield_after_complex(lines, *TAIL_YIELD) if TAIL_YIELD else lines
     if kmov:
         if "s_nop 0" in lines:
             lines[lines.index("s_nop 0")] = kmov
@@ -311,6 +311,10 @@ def tail_round(j):
             lines.insert(0, kmov)
     return lines
 
+
+# issue-yield pattern of the tail form (the product's: after every second
+# 4-cycle op); set_yield() changes it together with rounds_asm's (A/B builds).
+TAIL_YIELD = (COMPLEX, 2)
 
 # statements of the tail form: (first round, end round); the window words each
 # one touches are derived from its text (at most 29 operands per statement)
@@ -418,6 +422,22 @@ AB_VARIANTS = {
 }
 
 
+# --yield forms for A/B builds of the whole library (tools/yield_sweep.sh):
+# the request kernels' issue-yield density at 4 waves per SIMD.
+YIELD_FORMS = {
+    "1": (COMPLEX, 1), "2": (COMPLEX, 2), "3": (COMPLEX, 3), "4": (COMPLEX, 4),
+    "rot": (("v_alignbit_b32",), 1), "rot2": (("v_alignbit_b32",), 2), "none": False,
+}
+
+
+def set_yield(form):
+    global TAIL_YIELD
+    y = YIELD_FORMS[form]
+    ch, ad, km, _ = VARIANTS["rounds_asm"]
+    VARIANTS["rounds_asm"] = (ch, ad, km, y)
+    TAIL_YIELD = y
+
+
 def emit_fn(name, ch_mode, add_mode, k_mode, nops, rounds=(0, 64)):
     out = ["template <class H = NoHook>",
            f"__device__ __forceinline__ void {name}(uint32_t s[8], uint32_t w[16], H hook = {{}}) {{",
@@ -517,4 +537,6 @@ def emit_ab():
 if __name__ == "__main__":
     import sys
 
+    if "--yield" in sys.argv:  # A/B builds only; the product header is the default form
+        set_yield(sys.argv[sys.argv.index("--yield") + 1])
     sys.stdout.write(emit_ab() if "--ab" in sys.argv else emit())
