@@ -1182,7 +1182,8 @@ def main():
     props = torch.cuda.get_device_properties(dev)
     rank_info = {"rank": rank, "local_rank": local, "device": local,
                  "device_uuid": str(getattr(props, "uuid", "")), "pci_bus_id": getattr(props, "pci_bus_id", None),
-                 "digests": int(wl.digests), "wall_ms_per_step": dt_rank / a.steps * 1e3,
+                 "digests": int(wl.digests), "compressions": int(work_blocks),
+                 "first_request": int(getattr(wl, "first_req", 0)), "wall_ms_per_step": dt_rank / a.steps * 1e3,
                  "kernel": kname, "kernel_avg_launch_ms": ms_k / max(n_k, 1),
                  "frac": achieved_tops / VALU_PEAK_TOPS}
     per_rank = [rank_info]
