@@ -221,6 +221,9 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     uint64_t* soff = reinterpret_cast<uint64_t*>(mb);
     uint32_t* slen = reinterpret_cast<uint32_t*>(mb + 8ull * n);
     uint32_t* sord = slen + n;
+    // The metadata block is page-locked host memory: written once, never
+    // read back by the host (a second pass over it cost more than the first).
+    const uint64_t base = n ? off[0] : 0;
     mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
         Part& q = parts[a / step];
         for (uint32_t i = a; i < b; i++) {
@@ -230,7 +233,7 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
                 q.bad = i;
                 return;
             }
-            soff[i] = o;
+            soff[i] = o - base;  // rebased on off[0]; redone below if some offset lies before it
             slen[i] = L;
             q.lo = std::min(q.lo, o);
             q.hi = std::max(q.hi, o + L);
@@ -264,9 +267,9 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         return fail(c, MIRSHA_ERANGE, "submission of %llu bytes exceeds one device arena (%u); split it",
                     (unsigned long long)bytes, MIRSHA_MAX_DEVICE_ARENA_BYTES);
     if (dense) {
-        if (lo)
+        if (lo != base)  // an offset before off[0]: rebase on the true minimum, from the caller's array
             mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
-                for (uint32_t i = a; i < b; i++) soff[i] -= lo;
+                for (uint32_t i = a; i < b; i++) soff[i] = off[i] - lo;
             });
     } else {  // packed back to back: off = exclusive scan of len
         uint64_t p = 0;
@@ -275,7 +278,7 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
             p += len[i];
         }
     }
-    const bool identity = n == 0 || all.bmin == all.bmax || bucket_order(slen, n, sord);
+    const bool identity = n == 0 || all.bmin == all.bmax || bucket_order(len, n, sord);
     ph[MIRSHA_PROF_VALIDATE] = ms_since(t0);
     t0 = Clock::now();
     sl.rank.clear();
