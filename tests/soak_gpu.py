@@ -6,7 +6,8 @@ host arenas with gaps and odd alignments, sliced requests with duplicates
 digests (nulls, empty and shared lists) through the host call and through
 device plans in every mode, tile-queue count and list-tile form, overlapped
 cycles, launches of 65K-400K requests, fused plans with split tiles,
-checkpoint chains -- each checked bit for bit against the oracle (test infrastructure,
+checkpoint chains, arena submissions in random chunks (mirsha_submit_batch
+and its multi-device twin, page-locked or pageable arenas and outputs) -- each checked bit for bit against the oracle (test infrastructure,
 oracle/).  Prints a progress line every ~15 s; exits 1 at the first mismatch
 with the seed that reproduces it.
 
@@ -321,6 +322,41 @@ def case_multi(multi, rng, seed):
         check(np.array_equal(multi.wait(t), want), f"multi async n={n}", seed)
 
 
+def case_arena(eng, multi, pinned, rng, seed):
+    """mirsha_submit_batch / mirsha_submit_arena_multi: one cycle's arena (gaps,
+    overlaps, odd base) submitted in random chunks, page-locked or pageable
+    arena and digest buffer, sometimes a slice submission in between."""
+    n = int(rng.integers(1, 20000))
+    ln = lengths(rng, n)
+    arena, off = arena_for(rng, ln)
+    want = oracle_py.hash_requests(arena, off, ln, threads=8)
+    p_arena, p_out = pinned
+    if rng.random() < 0.5 and arena.size <= p_arena.size:
+        a = p_arena[: arena.size]
+        a[:] = arena
+    else:
+        a = arena
+    out = p_out[: 32 * n].reshape(n, 32) if rng.random() < 0.5 and 32 * n <= p_out.size else np.empty((n, 32), np.uint8)
+    out[:] = 0
+    use_multi = rng.random() < 0.3
+    e = multi if use_multi else eng
+    submit = e.submit_arena if use_multi else e.submit_batch
+    cuts = np.unique(np.concatenate([[0, n], rng.integers(0, n + 1, int(rng.integers(0, 12)))]))
+    tickets, extra = [], None
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        tickets.append(submit(a, off[lo:hi], ln[lo:hi], out=out[lo:hi]))
+        if not use_multi and extra is None and rng.random() < 0.2:
+            extra = (lo, hi, eng.submit_slices([[arena[int(o):int(o) + int(m)].tobytes()]
+                                                for o, m in zip(off[lo:hi], ln[lo:hi])]))
+    if tickets:
+        e.wait(tickets[int(rng.integers(0, len(tickets)))])
+        e.wait(tickets[-1])
+    check(np.array_equal(out, want), f"submit_arena multi={use_multi} n={n} chunks={len(tickets)}", seed)
+    if extra is not None:
+        lo, hi, t = extra
+        check(np.array_equal(eng.wait(t), want[lo:hi]), "slice submission between arena chunks", seed)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=120.0)
@@ -330,16 +366,20 @@ def main():
 
     eng = Engine(0)
     multi = MultiEngine([0, 0])
+    pinned = (multi.host_empty(64 << 20), multi.host_empty(32 * 20000))  # portable: both engines' devices
     t0 = last = time.time()
-    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0, "chains": 0, "split": 0, "multi": 0}
+    counts = {"host": 0, "slices": 0, "plan": 0, "large": 0, "chains": 0, "split": 0, "multi": 0, "arena": 0}
     k = 0
     while time.time() - t0 < a.seconds:
         seed = a.seed * 1_000_003 + k
         rng = np.random.default_rng(seed)
-        which = ("host", "slices", "plan", "host", "slices", "plan", "large", "chains", "split", "multi")[k % 10]
+        which = ("host", "slices", "plan", "arena", "host", "slices", "plan", "large", "chains", "split", "multi",
+                 "arena")[k % 12]
         try:
             if which == "multi":
                 case_multi(multi, rng, seed)
+            elif which == "arena":
+                case_arena(eng, multi, pinned, rng, seed)
             else:
                 {"host": case_host, "slices": case_slices, "plan": case_plan, "large": case_large,
                  "chains": case_chains, "split": case_split}[which](eng, rng, seed)

@@ -12,11 +12,20 @@ pytestmark = pytest.mark.gpu
 
 
 def test_random_shapes_15s(engine):
+    from mirbft_amd import MultiEngine
+
+    multi = MultiEngine([0, 0])
+    pinned = (multi.host_empty(64 << 20), multi.host_empty(32 * 20000))
+
+    def arena(eng, rng, seed):
+        soak_gpu.case_arena(eng, multi, pinned, rng, seed)
+
     cases = (soak_gpu.case_host, soak_gpu.case_slices, soak_gpu.case_plan, soak_gpu.case_large,
-             soak_gpu.case_chains)
+             soak_gpu.case_chains, arena)
     t0, k = time.time(), 0
     while time.time() - t0 < 15.0 or k < len(cases):
         seed = 23 * 1_000_003 + k
         cases[k % len(cases)](engine, np.random.default_rng(seed), seed)
         k += 1
+    multi.close()
     assert k >= len(cases)
