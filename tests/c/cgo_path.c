@@ -483,6 +483,16 @@ int main(int argc, char** argv) {
         CHECK(mirsha_hash_slices(ctx, sp, sl, sf, n, dig_l));
         leg_put(&lib, r, 0.0, now_ms() - t0);
     }
+    char lphases[256];
+    {
+        double lp[MIRSHA_PROF_PHASES] = {0};
+        mirsha_ctx_host_profile(ctx, lp, MIRSHA_PROF_PHASES);
+        snprintf(lphases, sizeof lphases,
+                 ", \"last_call_phases_ms\": {\"validate\": %.3f, \"plan\": %.3f, \"pack\": %.3f, \"device\": %.3f, "
+                 "\"scatter\": %.3f, \"total\": %.3f, \"chunks\": %.0f}",
+                 lp[MIRSHA_PROF_VALIDATE], lp[MIRSHA_PROF_PLAN], lp[MIRSHA_PROF_PACK], lp[MIRSHA_PROF_DEVICE],
+                 lp[MIRSHA_PROF_SCATTER], lp[MIRSHA_PROF_TOTAL], lp[MIRSHA_PROF_CHUNKS]);
+    }
     /* multi: GPUHasherMulti over every device (device 0 twice on one GPU) */
     int devs[16], nd = ndev > 1 ? (ndev < 16 ? ndev : 16) : 2;
     for (int k = 0; k < nd; k++) devs[k] = ndev > 1 ? k : 0;
@@ -514,7 +524,7 @@ int main(int argc, char** argv) {
     printf(", ");
     leg_print("onecall", &one, reps, n, "");
     printf(", ");
-    leg_print("lib", &lib, reps, n, "");
+    leg_print("lib", &lib, reps, n, lphases);
     printf(", ");
     leg_print("multi", &mul, reps, n, mextra);
     printf(", \"sample\": \"%s\"}\n", sample);
