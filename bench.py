@@ -962,6 +962,17 @@ def launch_ranks(a):
 
     fw = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
     fw.start()
+
+    def stop(signum, _frame):  # a launcher's time limit: take the ranks down with us
+        for q in procs:
+            if q.poll() is None:
+                q.terminate()
+        sys.exit(128 + signum)
+
+    import signal
+
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
     rc = 0
     live = list(range(n))
     while live:
@@ -995,6 +1006,8 @@ def launch_check(a, world, rank):
     if world > 1:
         dist.init_process_group("gloo")
         dist.barrier()
+    if os.environ.get("MIRSHA_BENCH_CHECK_SLEEP"):  # test hook: ranks that outlive a launcher's signal
+        time.sleep(float(os.environ["MIRSHA_BENCH_CHECK_SLEEP"]))
     n = a.requests or CONFIGS[a.config if a.config in CONFIGS else 2][1]
     info = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
             "first_request": rank * n, "requests": n}

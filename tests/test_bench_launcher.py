@@ -64,3 +64,31 @@ def test_failing_rank_fails_the_launch():
     r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"], MIRSHA_BENCH_DEVICE="0")
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_sigterm_to_the_launcher_stops_its_ranks():
+    """A driver's time limit signals the launching process: its ranks must not
+    outlive it (they would keep holding GPUs)."""
+    import signal
+    import time
+
+    import psutil
+
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--launch-check"],
+                         env=_env(MIRSHA_BENCH_CHECK_SLEEP="60"), stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        parent = psutil.Process(p.pid)
+        deadline = time.time() + 60
+        kids = []
+        while time.time() < deadline and len(kids) < 2:
+            kids = parent.children()
+            time.sleep(0.2)
+        assert len(kids) == 2, kids
+        time.sleep(1.0)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=30) == 128 + signal.SIGTERM
+        gone, alive = psutil.wait_procs(kids, timeout=30)
+        assert not alive, alive
+    finally:
+        if p.poll() is None:
+            p.kill()
