@@ -223,6 +223,34 @@ void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, ui
     pool().run(n, threads, fn);
 }
 
+uint64_t exclusive_scan(const uint32_t* len, uint32_t n, uint64_t* out) {
+    const int T = n < (1u << 16) ? 1 : std::min<int>(max_threads(), (int)(n >> 15));
+    if (T <= 1) {
+        uint64_t p = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            out[i] = p;
+            p += len[i];
+        }
+        return p;
+    }
+    const uint32_t step = (n + (uint32_t)T - 1) / (uint32_t)T;
+    std::vector<uint64_t> part(T + 1, 0);
+    parallel_for(n, T, [&](uint32_t a, uint32_t b) {
+        uint64_t s = 0;
+        for (uint32_t i = a; i < b; i++) s += len[i];
+        part[a / step + 1] = s;
+    });
+    for (int k = 1; k <= T; k++) part[k] += part[k - 1];
+    parallel_for(n, T, [&](uint32_t a, uint32_t b) {
+        uint64_t p = part[a / step];
+        for (uint32_t i = a; i < b; i++) {
+            out[i] = p;
+            p += len[i];
+        }
+    });
+    return part[T];
+}
+
 uint64_t fingerprint(const uint8_t* const* ptr, const uint64_t* len, uint32_t s0, uint32_t s1) {
     if (weak_fp()) return 0;
     Fp f;

@@ -25,6 +25,11 @@ int threads_for(uint64_t bytes, uint32_t n);
 // fn(lo, hi) over contiguous index ranges covering [0, n), on `threads` threads.
 void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, uint32_t)>& fn);
 
+// out[i] = len[0] + ... + len[i-1]; returns the total.  Two passes over
+// contiguous parts on the pool (part sums, then each part's offsets) when n is
+// large (a config-2 cycle's 2^20 lengths: ~1 ms serially).
+uint64_t exclusive_scan(const uint32_t* len, uint32_t n, uint64_t* out);
+
 // Host threads of the process: min(hardware threads, 16), or MIRSHA_HOST_THREADS.
 int max_threads();
 

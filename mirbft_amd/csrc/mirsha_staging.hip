@@ -677,11 +677,7 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
     // One packing pass, by threads, straight into pinned staging (the Go
     // side's single copy), chunk by chunk behind the DMA of the previous one.
     std::vector<uint64_t> poff(n);
-    uint64_t p = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        poff[i] = p;
-        p += len[i];
-    }
+    const uint64_t p = mirsha::host::exclusive_scan(len.data(), n, poff.data());
     ArenaSrc src;
     src.ptr = slice_ptr;
     src.slen = slice_len;
