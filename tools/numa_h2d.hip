@@ -121,6 +121,35 @@ int main(int argc, char** argv) {
         (void)hipHostUnregister(h);
         munmap(h, bytes);
     }
-    printf("]}\n");
+    // hipHostMalloc's own placement (what mirsha_host_alloc hands out)
+    {
+        void* h = nullptr;
+        if (hipHostMalloc(&h, bytes, hipHostMallocDefault) != hipSuccess) return 6;
+        memset(h, 7, bytes);
+        int where = -1;
+        {
+            long r = syscall(SYS_get_mempolicy, &where, nullptr, 0, h, 3 /* MPOL_F_NODE | MPOL_F_ADDR */);
+            if (r != 0) where = -1;
+        }
+        double bw[2];
+        for (int dir = 0; dir < 2; dir++) {
+            std::vector<double> t;
+            for (int r = 0; r < 10; r++) {
+                const double t0 = now();
+                if (dir == 0)
+                    (void)hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+                else
+                    (void)hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s);
+                (void)hipStreamSynchronize(s);
+                if (r) t.push_back(now() - t0);
+            }
+            std::sort(t.begin(), t.end());
+            bw[dir] = bytes / t[t.size() / 2] / 1e9;
+        }
+        printf("], \"hipHostMalloc\": {\"first_page_node\": %d, \"h2d_gbs\": %.1f, \"d2h_gbs\": %.1f}", where, bw[0],
+               bw[1]);
+        (void)hipHostFree(h);
+    }
+    printf("}\n");
     return 0;
 }
