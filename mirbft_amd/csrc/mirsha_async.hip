@@ -208,9 +208,9 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
                                  : (int)std::min<uint32_t>((uint32_t)mirsha::host::max_threads(), n / (1u << 16));
     std::vector<Part> parts(T);
     const uint32_t step = n ? (n + (uint32_t)T - 1) / (uint32_t)T : 1;
-    // staging: [request bytes (unless DMA'd from the caller) | off u64 | len u32 | order u32];
-    // the metadata block first goes at its offset for a copied arena, which needs
-    // the span; written at offset 0 of a separate region, then placed below.
+    // Slot buffers: `stage2` = the metadata block [off u64 | len u32 | order
+    // u32], `stage` = a copy of the request bytes when they are not DMA'd from
+    // the caller, `dev` = [request bytes + slack | metadata | digests].
     if (int rc = use_device(c)) return rc;
     AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
     if (sl.busy)
@@ -319,24 +319,35 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         sf[n] = n;
         mirsha::host::pack(sp.data(), sz.data(), sf.data(), nullptr, n, soff, st, mirsha::host::threads_for(bytes, n));
     }
-    if (n) {
-        if (!from_caller && bytes) HIP_TRY(c, hipMemcpyAsync(dv, st, bytes, hipMemcpyHostToDevice, c->xin));
-        HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, o_end, hipMemcpyHostToDevice, c->xin));
-        HIP_TRY(c, hipEventRecord(sl.ev_in, c->xin));
-        HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.ev_in, 0));
-        if (int rc = timed_launch(c, 0, [&] {
-                return mirsha::launch_msgs(dv, bytes, reinterpret_cast<const uint64_t*>(dv + d_meta),
-                                           reinterpret_cast<const uint32_t*>(dv + d_meta + o_len),
-                                           identity ? nullptr : reinterpret_cast<const uint32_t*>(dv + d_meta + o_ord),
-                                           n, dv + d_dig, c->variant, c->stream);
-            }))
-            return rc;
-        HIP_TRY(c, hipEventRecord(sl.ev_kern, c->stream));
-        HIP_TRY(c, hipStreamWaitEvent(c->xout, sl.ev_kern, 0));
-        HIP_TRY(c, hipMemcpyAsync(sl.direct ? out : sl.dig.as<uint8_t>(), dv + d_dig, 32ull * n, hipMemcpyDeviceToHost,
-                                  c->xout));
+    // Queue the copies and the kernel.  A failure part-way leaves work that
+    // reads this slot's buffers in flight while the slot is not marked busy:
+    // drain the three streams before reporting it.
+    auto queue = [&]() -> int {
+        if (n) {
+            if (!from_caller && bytes) HIP_TRY(c, hipMemcpyAsync(dv, st, bytes, hipMemcpyHostToDevice, c->xin));
+            HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, o_end, hipMemcpyHostToDevice, c->xin));
+            HIP_TRY(c, hipEventRecord(sl.ev_in, c->xin));
+            HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.ev_in, 0));
+            if (int rc = timed_launch(c, 0, [&] {
+                    return mirsha::launch_msgs(dv, bytes, reinterpret_cast<const uint64_t*>(dv + d_meta),
+                                               reinterpret_cast<const uint32_t*>(dv + d_meta + o_len),
+                                               identity ? nullptr
+                                                        : reinterpret_cast<const uint32_t*>(dv + d_meta + o_ord),
+                                               n, dv + d_dig, c->variant, c->stream);
+                }))
+                return rc;
+            HIP_TRY(c, hipEventRecord(sl.ev_kern, c->stream));
+            HIP_TRY(c, hipStreamWaitEvent(c->xout, sl.ev_kern, 0));
+            HIP_TRY(c, hipMemcpyAsync(sl.direct ? out : sl.dig.as<uint8_t>(), dv + d_dig, 32ull * n,
+                                      hipMemcpyDeviceToHost, c->xout));
+        }
+        HIP_TRY(c, hipEventRecord(sl.done, c->xout));
+        return MIRSHA_OK;
+    };
+    if (int rc = queue()) {
+        for (hipStream_t q : {c->xin, c->stream, c->xout}) (void)hipStreamSynchronize(q);
+        return rc;
     }
-    HIP_TRY(c, hipEventRecord(sl.done, c->xout));
     sl.t_queued = Clock::now();
     ph[MIRSHA_PROF_PACK] = ms_since(t0);
     sl.busy = true;
