@@ -194,36 +194,40 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
                        const uint32_t* len, uint32_t n, uint8_t* out, uint64_t* ticket_out) {
     auto t0 = Clock::now();
     double ph[MIRSHA_PROF_PHASES] = {};
-    // One pass over the n entries: bounds, the span [lo, hi), total bytes,
-    // block-count range; off / len copied into the metadata staging on the
-    // way (rebased below).  A chunk of the Go binding's HashBatch is ~60k
-    // requests and its goroutines are packing the NEXT chunk meanwhile, so
-    // the pass stays on the calling thread up to 2^18 requests (a pass per
-    // concern, with pool dispatches, cost ~0.2 ms per chunk).
+    // One pass over the n entries on the calling thread (up to 2^18
+    // requests: a chunk of the Go binding's HashBatch is ~120k requests and
+    // its goroutines pack the NEXT chunk meanwhile): bounds, the span [lo,
+    // hi), total bytes, block-count range, whether the requests are gapless,
+    // and the lengths into the metadata block.  Offsets cross PCIe only when
+    // the requests are not gapless (else the device rebuilds them by a scan
+    // of the lengths), the bucket order only when block counts differ: 4 B
+    // per request instead of 16 in the common case (the metadata shares the
+    // link with the request bytes and the digests).
     struct Part {
         uint64_t lo = UINT64_MAX, hi = 0, tot = 0;
         uint32_t bmin = UINT32_MAX, bmax = 0, bad = UINT32_MAX;
+        bool gapless = true;
     };
     const int T = n < (1u << 18) ? 1
                                  : (int)std::min<uint32_t>((uint32_t)mirsha::host::max_threads(), n / (1u << 16));
     std::vector<Part> parts(T);
     const uint32_t step = n ? (n + (uint32_t)T - 1) / (uint32_t)T : 1;
-    // Slot buffers: `stage2` = the metadata block [off u64 | len u32 | order
-    // u32], `stage` = a copy of the request bytes when they are not DMA'd from
-    // the caller, `dev` = [request bytes + slack | metadata | digests].
+    // Slot buffers: `stage2` = the metadata block [len u32 | order u32 | off
+    // u64] (the device's copy has the same layout), `stage` = a copy of the
+    // request bytes when they are not DMA'd from the caller, `dev` = [request
+    // bytes + slack | metadata | digests].
     if (int rc = use_device(c)) return rc;
     AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
     if (sl.busy)
         if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
-    const uint64_t meta_bytes = align8(16ull * n);
-    HIP_TRY(c, sl.stage2.ensure(std::max<uint64_t>(meta_bytes, 8)));  // metadata block of arena submissions
+    const uint64_t o_len = 0, o_ord = align8(4ull * n), o_off = align8(o_ord + 4ull * n), o_end = o_off + 8ull * n;
+    HIP_TRY(c, sl.stage2.ensure(std::max<uint64_t>(o_end, 8)));
     uint8_t* mb = sl.stage2.as<uint8_t>();
-    uint64_t* soff = reinterpret_cast<uint64_t*>(mb);
-    uint32_t* slen = reinterpret_cast<uint32_t*>(mb + 8ull * n);
-    uint32_t* sord = slen + n;
+    uint32_t* slen = reinterpret_cast<uint32_t*>(mb + o_len);
+    uint32_t* sord = reinterpret_cast<uint32_t*>(mb + o_ord);
+    uint64_t* soff = reinterpret_cast<uint64_t*>(mb + o_off);
     // The metadata block is page-locked host memory: written once, never
-    // read back by the host (a second pass over it cost more than the first).
-    const uint64_t base = n ? off[0] : 0;
+    // read back by the host.
     mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
         Part& q = parts[a / step];
         for (uint32_t i = a; i < b; i++) {
@@ -233,8 +237,8 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
                 q.bad = i;
                 return;
             }
-            soff[i] = o - base;  // rebased on off[0]; redone below if some offset lies before it
             slen[i] = L;
+            if (i > a && o != off[i - 1] + len[i - 1]) q.gapless = false;
             q.lo = std::min(q.lo, o);
             q.hi = std::max(q.hi, o + L);
             q.tot += L;
@@ -244,13 +248,17 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         }
     });
     Part all;
-    for (const Part& q : parts) {
+    for (int k = 0; k < T; k++) {
+        const Part& q = parts[k];
         all.bad = std::min(all.bad, q.bad);
         all.lo = std::min(all.lo, q.lo);
         all.hi = std::max(all.hi, q.hi);
         all.tot += q.tot;
         all.bmin = std::min(all.bmin, q.bmin);
         all.bmax = std::max(all.bmax, q.bmax);
+        all.gapless = all.gapless && q.gapless;
+        const uint32_t a = (uint32_t)k * step;  // part boundaries
+        if (k > 0 && a < n && off[a] != off[a - 1] + len[a - 1]) all.gapless = false;
     }
     if (all.bad != UINT32_MAX) {
         const uint32_t i = all.bad;
@@ -266,12 +274,13 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     if (bytes + kArenaSlack > MIRSHA_MAX_DEVICE_ARENA_BYTES)
         return fail(c, MIRSHA_ERANGE, "submission of %llu bytes exceeds one device arena (%u); split it",
                     (unsigned long long)bytes, MIRSHA_MAX_DEVICE_ARENA_BYTES);
-    if (dense) {
-        if (lo != base)  // an offset before off[0]: rebase on the true minimum, from the caller's array
-            mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
-                for (uint32_t i = a; i < b; i++) soff[i] = off[i] - lo;
-            });
-    } else {  // packed back to back: off = exclusive scan of len
+    // gapless => in order from lo = off[0]: the device scan of the lengths is the offsets
+    const bool gapless = n && dense && all.gapless;
+    if (!gapless && dense) {
+        mirsha::host::parallel_for(n, T, [&](uint32_t a, uint32_t b) {
+            for (uint32_t i = a; i < b; i++) soff[i] = off[i] - lo;
+        });
+    } else if (!dense) {  // packed back to back: off = exclusive scan of len
         uint64_t p = 0;
         for (uint32_t i = 0; i < n; i++) {
             soff[i] = p;
@@ -279,6 +288,8 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         }
     }
     const bool identity = n == 0 || all.bmin == all.bmax || bucket_order(len, n, sord);
+    // bytes of the metadata block that cross PCIe
+    const uint64_t meta_copy = !gapless ? o_end : !identity ? o_ord + 4ull * n : 4ull * n;
     ph[MIRSHA_PROF_VALIDATE] = ms_since(t0);
     t0 = Clock::now();
     sl.rank.clear();
@@ -293,9 +304,13 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     const bool from_caller = dense && n && host_pinned(arena + lo);
     sl.direct = host_pinned(out);
     if (!sl.direct) HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
-    // device: [request bytes + slack | off u64 | len u32 | order u32 | digests]
-    const uint64_t o_len = 8ull * n, o_ord = o_len + 4ull * n, o_end = meta_bytes;
+    // device: [request bytes + slack | len u32 | order u32 | off u64 | digests]
     const uint64_t d_meta = align8(bytes + kArenaSlack), d_dig = d_meta + o_end;
+    size_t scan_bytes = 0;
+    if (gapless) {
+        HIP_TRY(c, mirsha::launch_offsets_scan(nullptr, scan_bytes, nullptr, nullptr, n, c->stream));
+        HIP_TRY(c, c->d_scan.ensure(std::max<size_t>(scan_bytes, 4)));
+    }
     if (!from_caller) HIP_TRY(c, sl.stage.ensure(std::max<uint64_t>(bytes, 8)));
     HIP_TRY(c, sl.dev.ensure(d_dig + 32ull * n));
     uint8_t* st = sl.stage.as<uint8_t>();
@@ -325,12 +340,15 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     auto queue = [&]() -> int {
         if (n) {
             if (!from_caller && bytes) HIP_TRY(c, hipMemcpyAsync(dv, st, bytes, hipMemcpyHostToDevice, c->xin));
-            HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, o_end, hipMemcpyHostToDevice, c->xin));
+            HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, meta_copy, hipMemcpyHostToDevice, c->xin));
             HIP_TRY(c, hipEventRecord(sl.ev_in, c->xin));
             HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.ev_in, 0));
+            uint64_t* d_off = reinterpret_cast<uint64_t*>(dv + d_meta + o_off);
+            const uint32_t* d_len = reinterpret_cast<const uint32_t*>(dv + d_meta + o_len);
+            if (gapless)  // off = exclusive scan of len, on the device (c->d_scan: c->stream's scratch)
+                HIP_TRY(c, mirsha::launch_offsets_scan(c->d_scan.p, scan_bytes, d_len, d_off, n, c->stream));
             if (int rc = timed_launch(c, 0, [&] {
-                    return mirsha::launch_msgs(dv, bytes, reinterpret_cast<const uint64_t*>(dv + d_meta),
-                                               reinterpret_cast<const uint32_t*>(dv + d_meta + o_len),
+                    return mirsha::launch_msgs(dv, bytes, d_off, d_len,
                                                identity ? nullptr
                                                         : reinterpret_cast<const uint32_t*>(dv + d_meta + o_ord),
                                                n, dv + d_dig, c->variant, c->stream);

@@ -296,11 +296,13 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
     const uint64_t total = offsets_parallel(reqs, n, off, lens, pool);
     ph_off = now_ms() - t0;
     ph_pack = ph_submit = 0.0;
-    /* chunk boundaries: requests [lo, hi) until the chunk's bytes reach chunk_bytes */
+    /* chunk boundaries: requests [lo, hi) until the chunk's bytes reach the
+     * budget (a quarter of it for the first chunk, so the DMA starts early) */
     int nk = 0;
     for (uint32_t lo = 0; lo < n;) {
+        const uint64_t budget = nk ? chunk_bytes : chunk_bytes / 4;
         uint32_t hi = lo + 1;
-        while (hi < n && off[hi] - off[lo] < chunk_bytes) hi++;
+        while (hi < n && off[hi] - off[lo] < budget) hi++;
         if (nk == MAX_CHUNKS) exit(6);
         cfirst[nk++] = lo;
         lo = hi;

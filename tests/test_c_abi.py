@@ -61,7 +61,7 @@ def test_cgo_path_on_gpu(tmp_path):
     round 4's one-call form, the serial form, the library-packed
     mirsha_hash_slices and the multi-device twin (mirsha_submit_arena_multi,
     device 0 twice): every leg agrees with the serial one (checked in the
-    program) and the digests are the oracle's.  A 1 MiB chunk budget gives 26
+    program) and the digests are the oracle's.  A 1 MiB chunk budget gives 27
     chunks, far more than the 4-slot ring."""
     exe = build(tmp_path, PATH_SRC, "cgo_path")
     n, data_len = 100_003, 256
@@ -69,8 +69,9 @@ def test_cgo_path_on_gpu(tmp_path):
     assert r.returncode == 0, r.stderr
     line = json.loads(r.stdout.splitlines()[-1])
     assert line["requests"] == n and line["parallel"]["ms"] > 0
-    per = -(-(1 << 20) // (16 + data_len))  # requests per 1 MiB chunk (the chunk ends at a request boundary)
-    assert line["parallel"]["chunks"] == -(-n // per) == line["multi"]["chunks"] == 26
+    # requests per chunk (a chunk ends at a request boundary; the first has a quarter of the budget)
+    per, first = -(-(1 << 20) // (16 + data_len)), -(-(1 << 18) // (16 + data_len))
+    assert line["parallel"]["chunks"] == 1 + -(-(n - first) // per) == line["multi"]["chunks"] == 27
     arena = oracle_py.gen_requests(0x6D69726266740002, 0, 4, data_len)
     stride = 16 + data_len
     want = oracle_py.hash_requests(arena, np.arange(4, dtype=np.uint64) * stride, np.full(4, stride))
