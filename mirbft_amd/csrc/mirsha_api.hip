@@ -4,11 +4,6 @@
 // mirsha_ctx.h.
 #include "mirsha_ctx.h"
 
-#include <sys/syscall.h>
-#include <unistd.h>
-
-#include <cctype>
-
 namespace mirsha_api {
 
 int fail(mirsha_ctx* c, int code, const char* fmt, ...) {
@@ -91,23 +86,6 @@ int check_lists(mirsha_ctx* c, const uint32_t* idx, const uint32_t* first, uint3
         if ((uint64_t)(first[b + 1] - first[b]) * 32u > MIRSHA_MAX_MESSAGE_BYTES)
             return fail(c, MIRSHA_ERANGE, "list %u too long", b);
     return MIRSHA_OK;
-}
-
-// NUMA node of a device's PCI function (sysfs), or -1.
-int device_numa_node(int device) {
-    char bus[64] = {0};
-    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
-        (void)hipGetLastError();
-        return -1;
-    }
-    for (char* p = bus; *p; p++) *p = (char)tolower(*p);
-    std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
-    int node = -1;
-    if (FILE* f = fopen(path.c_str(), "r")) {
-        if (fscanf(f, "%d", &node) != 1) node = -1;
-        fclose(f);
-    }
-    return node >= 0 && node < 1024 ? node : -1;
 }
 
 }  // namespace mirsha_api
@@ -252,27 +230,6 @@ int mirsha_host_alloc(mirsha_ctx* c, uint64_t bytes, void** out) {
     if (!c || !out) return MIRSHA_EINVAL;
     *out = nullptr;
     if (int rc = use_device(c)) return rc;
-    // A/B (MIRSHA_AB=1 MIRSHA_HOST_NUMA=1): pages on the GPU's NUMA node
-    // (sysfs numa_node of its PCI function) through the thread's memory
-    // policy and hipHostMallocNumaUser; tools/numa_h2d.hip measures whether
-    // the node matters on a box.
-    const int node = getenv_flag("MIRSHA_HOST_NUMA") ? device_numa_node(c->device) : -1;
-    if (node >= 0) {
-        int old_mode = 0;
-        unsigned long old_mask[16] = {0};
-        const bool saved = syscall(SYS_get_mempolicy, &old_mode, old_mask, 1024, nullptr, 0) == 0;
-        unsigned long mask[16] = {0};
-        mask[node / 64] = 1ul << (node % 64);
-        (void)syscall(SYS_set_mempolicy, 1 /* MPOL_PREFERRED */, mask, 1024);
-        const hipError_t e = hipHostMalloc(out, std::max<uint64_t>(bytes, 1), hipHostMallocNumaUser);
-        (void)syscall(SYS_set_mempolicy, saved ? old_mode : 0, saved ? old_mask : nullptr, saved ? 1024 : 0);
-        if (e != hipSuccess) {
-            *out = nullptr;
-            return fail(c, e == hipErrorOutOfMemory ? MIRSHA_ENOMEM : MIRSHA_EHIP, "hipHostMalloc (NUMA node %d): %s",
-                        node, hipGetErrorString(e));
-        }
-        return MIRSHA_OK;
-    }
     HIP_TRY(c, hipHostMalloc(out, std::max<uint64_t>(bytes, 1), hipHostMallocDefault));
     return MIRSHA_OK;
 }
