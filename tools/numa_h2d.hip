@@ -148,6 +148,27 @@ int main(int argc, char** argv) {
         }
         printf("], \"hipHostMalloc\": {\"first_page_node\": %d, \"h2d_gbs\": %.1f, \"d2h_gbs\": %.1f}", where, bw[0],
                bw[1]);
+        // Full duplex?  H2D of the whole buffer on one stream while D2H of
+        // 1/8 of it (the digests' share of a chunk) runs on another.
+        void* h2 = nullptr;
+        void* d2 = nullptr;
+        hipStream_t s2;
+        (void)hipStreamCreate(&s2);
+        if (hipHostMalloc(&h2, bytes / 8, hipHostMallocDefault) == hipSuccess && hipMalloc(&d2, bytes / 8) == hipSuccess) {
+            std::vector<double> t;
+            for (int r = 0; r < 10; r++) {
+                const double t0 = now();
+                (void)hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+                (void)hipMemcpyAsync(h2, d2, bytes / 8, hipMemcpyDeviceToHost, s2);
+                (void)hipStreamSynchronize(s);
+                (void)hipStreamSynchronize(s2);
+                if (r) t.push_back(now() - t0);
+            }
+            std::sort(t.begin(), t.end());
+            const double both = t[t.size() / 2];
+            printf(", \"duplex\": {\"h2d_plus_eighth_d2h_ms\": %.3f, \"h2d_alone_ms\": %.3f, \"serial_estimate_ms\": %.3f}",
+                   both * 1e3, bytes / (bw[0] * 1e9) * 1e3, (bytes / (bw[0] * 1e9) + bytes / 8 / (bw[1] * 1e9)) * 1e3);
+        }
         (void)hipHostFree(h);
     }
     printf("}\n");
