@@ -303,18 +303,6 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
     const bool from_caller = dense && n && host_pinned(arena + lo);
     sl.direct = host_pinned(out);
-    // A/B (MIRSHA_AB=1 MIRSHA_ASYNC_KERNEL_STORE=1): the kernel stores the
-    // digests straight into a page-locked digests_out over PCIe (posted
-    // writes) instead of a D2H copy that shares the copy engine with the next
-    // chunks' H2D.
-    uint8_t* kout = nullptr;
-    if (sl.direct && n && getenv_flag("MIRSHA_ASYNC_KERNEL_STORE")) {
-        void* dp = nullptr;
-        if (hipHostGetDevicePointer(&dp, out, 0) == hipSuccess)
-            kout = static_cast<uint8_t*>(dp);
-        else
-            (void)hipGetLastError();
-    }
     if (!sl.direct) HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
     // device: [request bytes + slack | len u32 | order u32 | off u64 | digests]
     const uint64_t d_meta = align8(bytes + kArenaSlack), d_dig = d_meta + o_end;
@@ -363,13 +351,9 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
                     return mirsha::launch_msgs(dv, bytes, d_off, d_len,
                                                identity ? nullptr
                                                         : reinterpret_cast<const uint32_t*>(dv + d_meta + o_ord),
-                                               n, kout ? kout : dv + d_dig, c->variant, c->stream);
+                                               n, dv + d_dig, c->variant, c->stream);
                 }))
                 return rc;
-            if (kout) {  // the digests are in host memory when the kernel ends
-                HIP_TRY(c, hipEventRecord(sl.done, c->stream));
-                return MIRSHA_OK;
-            }
             HIP_TRY(c, hipEventRecord(sl.ev_kern, c->stream));
             HIP_TRY(c, hipStreamWaitEvent(c->xout, sl.ev_kern, 0));
             HIP_TRY(c, hipMemcpyAsync(sl.direct ? out : sl.dig.as<uint8_t>(), dv + d_dig, 32ull * n,
