@@ -20,7 +20,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <immintrin.h>
 
 static long mbind_(void* addr, unsigned long len, int mode, const unsigned long* mask, unsigned long maxnode,
                    unsigned flags) {
@@ -168,6 +171,36 @@ int main(int argc, char** argv) {
             const double both = t[t.size() / 2];
             printf(", \"duplex\": {\"h2d_plus_eighth_d2h_ms\": %.3f, \"h2d_alone_ms\": %.3f, \"serial_estimate_ms\": %.3f}",
                    both * 1e3, bytes / (bw[0] * 1e9) * 1e3, (bytes / (bw[0] * 1e9) + bytes / 8 / (bw[1] * 1e9)) * 1e3);
+        }
+        // Freshly written buffers: 15 threads write the whole buffer (plain
+        // stores, or non-temporal stores that bypass the caches), then the
+        // H2D starts at once: does DMA of lines still dirty in CPU caches
+        // run slower?
+        for (int nt = 0; nt < 2; nt++) {
+            std::vector<double> t;
+            for (int r = 0; r < 10; r++) {
+                std::vector<std::thread> th;
+                const size_t per = bytes / 15 / 64 * 64;
+                for (int k = 0; k < 15; k++)
+                    th.emplace_back([&, k] {
+                        uint8_t* p = (uint8_t*)h + per * k;
+                        const size_t len = k == 14 ? bytes - per * 14 : per;
+                        if (!nt) {
+                            memset(p, r + k, len);
+                        } else {
+                            const __m128i v = _mm_set1_epi8((char)(r + k));
+                            for (size_t x = 0; x + 16 <= len; x += 16) _mm_stream_si128((__m128i*)(p + x), v);
+                            _mm_sfence();
+                        }
+                    });
+                for (auto& x : th) x.join();
+                const double t0 = now();
+                (void)hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, s);
+                (void)hipStreamSynchronize(s);
+                if (r) t.push_back(now() - t0);
+            }
+            std::sort(t.begin(), t.end());
+            printf(", \"%s\": {\"h2d_gbs\": %.1f}", nt ? "fresh_nontemporal" : "fresh_plain", bytes / t[t.size() / 2] / 1e9);
         }
         (void)hipHostFree(h);
     }
