@@ -423,14 +423,16 @@ class BatchWorkload:
         if not os.path.exists(exe):
             return {"note": f"{exe} not built (__graft_entry__.build())"}
         # 15 packing workers + the submitting thread = the GPU box's 16-CPU share
-        r = subprocess.run([exe, str(self.n), str(self.data_len), "15", "7", "32"], capture_output=True, text=True,
-                           timeout=300)
+        # "nt": the workers stream the arena with non-temporal stores (INTEGRATION.md streamPack)
+        r = subprocess.run([exe, str(self.n), str(self.data_len), "15", "7", "32", "nt"], capture_output=True,
+                           text=True, timeout=300)
         if r.returncode != 0:
             return {"error": r.stderr[-500:]}
         out = json.loads(r.stdout.splitlines()[-1])
         out.pop("sample", None)
         out["note"] = ("INTEGRATION.md GPUHasher.HashBatch made from C: 'parallel' = the chunked form (15 workers "
-                       "pack chunk k+1 while the caller submits chunk k, mirsha_submit_batch: DMA / kernel / D2H on "
+                       "pack chunk k+1 with non-temporal stores while the caller submits chunk k, "
+                       "mirsha_submit_batch: DMA / kernel / D2H on "
                        "three streams; digests DMA'd into a pinned buffer, copied to the Go-owned result by the "
                        "workers), 'onecall' = pack "
                        "everything then one mirsha_hash_batch, 'serial' = one goroutine packs, 'lib' = "

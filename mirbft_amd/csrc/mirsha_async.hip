@@ -95,7 +95,7 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
         HIP_TRY(c, dev.ensure(o_dig + 32ull * std::max<uint32_t>(m, 1)));
         uint8_t* st = stage.as<uint8_t>();
         mirsha::host::pack(slice_ptr, slice_len, slice_first, ids, m, poff.data(), st,
-                           mirsha::host::threads_for(bytes, m));
+                           mirsha::host::threads_for(bytes, m), true);
         memcpy(st + o_off, poff.data(), 8ull * m);
         memcpy(st + o_len, plen.data(), 4ull * m);
         const bool identity = bucket_order(plen.data(), m, reinterpret_cast<uint32_t*>(st + o_ord));
@@ -321,7 +321,7 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         HIP_TRY(c, hipMemcpyAsync(dv, arena + lo, bytes, hipMemcpyHostToDevice, c->xin));
     } else if (dense) {
         mirsha::host::pack_range(arena + lo, nullptr, nullptr, nullptr, 0, nullptr, 0, bytes, st,
-                                 mirsha::host::threads_for(bytes, 1u << 20));
+                                 mirsha::host::threads_for(bytes, 1u << 20), true);
     } else {
         std::vector<const uint8_t*> sp(n);
         std::vector<uint64_t> sz(n);
@@ -332,7 +332,8 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
             sf[i] = i;
         }
         sf[n] = n;
-        mirsha::host::pack(sp.data(), sz.data(), sf.data(), nullptr, n, soff, st, mirsha::host::threads_for(bytes, n));
+        mirsha::host::pack(sp.data(), sz.data(), sf.data(), nullptr, n, soff, st, mirsha::host::threads_for(bytes, n),
+                           true);
     }
     // Queue the copies and the kernel.  A failure part-way leaves work that
     // reads this slot's buffers in flight while the slot is not marked busy:

@@ -5,6 +5,7 @@
 
 #include <stdlib.h>
 #include <string.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -563,9 +564,74 @@ uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32
     return d.resolve(rep, nullptr);
 }
 
+namespace {
+// memcpy whose body bypasses the CPU caches (16-byte non-temporal stores):
+// page-locked staging written this way DMAs at the link's 57.4 GB/s, written
+// with plain stores at 52.4 (the lines are still dirty in CPU caches when the
+// copy engine reads them; profiles/r05o).  Head and tail are plain stores.
+// The caller fences (_mm_sfence) before the DMA may start.
+void stream_copy(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    uint64_t h = (16 - ((uintptr_t)dst & 15)) & 15;
+    if (h > n) h = n;
+    if (h) memcpy(dst, src, h);
+    dst += h, src += h, n -= h;
+    for (; n >= 64; n -= 64, dst += 64, src += 64) {
+        const __m128i x0 = _mm_loadu_si128((const __m128i*)src), x1 = _mm_loadu_si128((const __m128i*)(src + 16)),
+                      x2 = _mm_loadu_si128((const __m128i*)(src + 32)), x3 = _mm_loadu_si128((const __m128i*)(src + 48));
+        _mm_stream_si128((__m128i*)dst, x0);
+        _mm_stream_si128((__m128i*)(dst + 16), x1);
+        _mm_stream_si128((__m128i*)(dst + 32), x2);
+        _mm_stream_si128((__m128i*)(dst + 48), x3);
+    }
+    for (; n >= 16; n -= 16, dst += 16, src += 16) _mm_stream_si128((__m128i*)dst, _mm_loadu_si128((const __m128i*)src));
+    if (n) memcpy(dst, src, n);
+}
+
+// Gathers small pieces into a cache-resident window and streams the window
+// out whole; pieces of a window's size or more stream directly.
+struct StreamWriter {
+    static constexpr uint64_t kWin = 16384;
+    alignas(64) uint8_t win[kWin];
+    uint8_t* at = nullptr;  // destination of win[0]
+    uint64_t fill = 0;
+    void flush() {
+        if (fill) stream_copy(at, win, fill);
+        fill = 0;
+    }
+    void put(uint8_t* d, const uint8_t* s, uint64_t n) {
+        if (!n) return;
+        if (fill && (d != at + fill || fill + n > kWin)) flush();
+        if (n >= kWin) {
+            stream_copy(d, s, n);
+            return;
+        }
+        if (!fill) at = d;
+        memcpy(win + fill, s, n);
+        fill += n;
+    }
+    void done() {
+        flush();
+        _mm_sfence();
+    }
+};
+}  // namespace
+
 void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,
-          uint32_t m, const uint64_t* dst_off, uint8_t* dst, int threads) {
+          uint32_t m, const uint64_t* dst_off, uint8_t* dst, int threads, bool stream) {
     parallel_for(m, threads, [&](uint32_t lo, uint32_t hi) {
+        if (stream) {
+            StreamWriter w;
+            for (uint32_t k = lo; k < hi; k++) {
+                const uint32_t i = which ? which[k] : k;
+                uint8_t* d = dst + dst_off[k];
+                for (uint32_t s = first[i]; s < first[i + 1]; s++) {
+                    w.put(d, ptr[s], len[s]);
+                    d += len[s];
+                }
+            }
+            w.done();
+            return;
+        }
         for (uint32_t k = lo; k < hi; k++) {
             const uint32_t i = which ? which[k] : k;
             uint8_t* d = dst + dst_off[k];
@@ -580,7 +646,7 @@ void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first,
 namespace {
 // Sequential body of pack_range over [a, b).
 void pack_range_seq(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
-                    const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst) {
+                    const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst, StreamWriter* w) {
     if (a >= b) return;
     // last request starting at or before a (poff nondecreasing)
     uint32_t i = (uint32_t)(std::upper_bound(poff, poff + n, a) - poff);
@@ -590,7 +656,12 @@ void pack_range_seq(const uint8_t* const* ptr, const uint64_t* len, const uint32
         for (uint32_t sl = first[i]; sl < first[i + 1] && p < b; sl++) {
             const uint64_t L = len[sl];
             const uint64_t lo = std::max(p, a), hi = std::min(p + L, b);
-            if (lo < hi) memcpy(dst + (lo - a), ptr[sl] + (lo - p), hi - lo);
+            if (lo < hi) {
+                if (w)
+                    w->put(dst + (lo - a), ptr[sl] + (lo - p), hi - lo);
+                else
+                    memcpy(dst + (lo - a), ptr[sl] + (lo - p), hi - lo);
+            }
             p += L;
         }
     }
@@ -598,7 +669,7 @@ void pack_range_seq(const uint8_t* const* ptr, const uint64_t* len, const uint32
 }  // namespace
 
 void pack_range(const uint8_t* base, const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first,
-                uint32_t n, const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst, int threads) {
+                uint32_t n, const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst, int threads, bool stream) {
     if (a >= b) return;
     const uint64_t total = b - a;
     if (threads < 1) threads = 1;
@@ -607,10 +678,18 @@ void pack_range(const uint8_t* base, const uint8_t* const* ptr, const uint64_t* 
         for (uint32_t t = lo; t < hi; t++) {
             const uint64_t x = a + std::min<uint64_t>(total, piece * t), y = a + std::min<uint64_t>(total, piece * (t + 1));
             if (x >= y) continue;
-            if (!ptr)
+            if (!ptr && !stream) {
                 memcpy(dst + (x - a), base + x, y - x);
-            else
-                pack_range_seq(ptr, len, first, n, poff, x, y, dst + (x - a));
+            } else if (!ptr) {
+                stream_copy(dst + (x - a), base + x, y - x);
+                _mm_sfence();
+            } else if (!stream) {
+                pack_range_seq(ptr, len, first, n, poff, x, y, dst + (x - a), nullptr);
+            } else {
+                StreamWriter w;
+                pack_range_seq(ptr, len, first, n, poff, x, y, dst + (x - a), &w);
+                w.done();
+            }
         }
     });
 }

@@ -112,18 +112,23 @@ class DedupScan {
 uint32_t dedup_plan(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, uint32_t n,
                     uint32_t* rep, const uint8_t** err_out, std::vector<uint8_t>* err);
 
-// Copies request which[k] (k < m) to dst + dst_off[k], in parallel.
+// Copies request which[k] (k < m) to dst + dst_off[k], in parallel.  With
+// `stream` the stores bypass the CPU caches (non-temporal, fenced before
+// return): for page-locked staging a DMA reads next, which then runs at the
+// link's rate instead of ~9% below it (profiles/r05o).  Not for buffers the
+// CPU reads back.
 void pack(const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first, const uint32_t* which,
-          uint32_t m, const uint64_t* dst_off, uint8_t* dst, int threads);
+          uint32_t m, const uint64_t* dst_off, uint8_t* dst, int threads, bool stream = false);
 
 // Bytes [a, b) of the packed arena of n requests -- request i = concat of its
 // slices [first[i], first[i+1]), placed at poff[i] (nondecreasing) -- into
 // dst (dst[0] = byte a), split over `threads` threads by byte range.  With
 // ptr == nullptr the source is the contiguous `base` instead (a parallel
 // memcpy of base[a, b)).  Used to fill one pinned staging chunk while the
-// previous chunk's DMA is in flight.
+// previous chunk's DMA is in flight.  `stream` as for pack.
 void pack_range(const uint8_t* base, const uint8_t* const* ptr, const uint64_t* len, const uint32_t* first,
-                uint32_t n, const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst, int threads);
+                uint32_t n, const uint64_t* poff, uint64_t a, uint64_t b, uint8_t* dst, int threads,
+                bool stream = false);
 
 }  // namespace host
 }  // namespace mirsha

@@ -37,7 +37,7 @@ void pmemcpy(void* dst, const void* src, uint64_t n) {
 
 void fill(const ArenaSrc& src, uint64_t a, uint64_t b, uint8_t* dst) {
     mirsha::host::pack_range(src.base, src.ptr, src.slen, src.sfirst, src.n, src.poff, a, b, dst,
-                             mirsha::host::threads_for(b - a, 1u << 20));
+                             mirsha::host::threads_for(b - a, 1u << 20), true);
 }
 
 // Queues src's bytes into d_arena on c->stream (large arenas; small ones are

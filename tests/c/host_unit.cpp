@@ -72,7 +72,7 @@ static void test_pack(std::mt19937_64& rng) {
         poff[i] = want.size();
         const int k = (int)(rng() % 4);
         for (int s = 0; s < k; s++) {
-            const uint64_t l = (rng() % 5 == 0) ? 0 : rng() % 700;
+            const uint64_t l = (rng() % 5 == 0) ? 0 : (rng() % 60 == 0) ? rng() % 40000 : rng() % 700;
             const uint64_t o = rng() % (buf.size() - l);
             ptr.push_back(buf.data() + o);
             len.push_back(l);
@@ -82,11 +82,12 @@ static void test_pack(std::mt19937_64& rng) {
         rlen[i] = want.size() - poff[i];
     }
     const uint64_t total = want.size();
-    for (int t : {1, 4, 16}) {
-        std::vector<uint8_t> got(total, 0xAA);
-        pack(ptr.data(), len.data(), first.data(), nullptr, n, poff.data(), got.data(), t);
-        EXPECT(got == want, "pack with %d threads", t);
-    }
+    for (int t : {1, 4, 16})
+        for (bool stream : {false, true}) {
+            std::vector<uint8_t> got(total, 0xAA);
+            pack(ptr.data(), len.data(), first.data(), nullptr, n, poff.data(), got.data(), t, stream);
+            EXPECT(got == want, "pack with %d threads (stream %d)", t, (int)stream);
+        }
     // a subset in another order, packed densely
     std::vector<uint32_t> which;
     for (uint32_t i = 0; i < n; i += 3) which.push_back(n - 1 - i);
@@ -98,23 +99,32 @@ static void test_pack(std::mt19937_64& rng) {
         p += rlen[which[k]];
         wwant.insert(wwant.end(), want.begin() + (long)poff[which[k]], want.begin() + (long)(poff[which[k]] + rlen[which[k]]));
     }
-    std::vector<uint8_t> wgot(p, 0);
-    pack(ptr.data(), len.data(), first.data(), which.data(), (uint32_t)which.size(), woff.data(), wgot.data(), 8);
-    EXPECT(wgot == wwant, "pack of a reordered subset");
+    for (bool stream : {false, true}) {
+        std::vector<uint8_t> wgot(p, 0);
+        pack(ptr.data(), len.data(), first.data(), which.data(), (uint32_t)which.size(), woff.data(), wgot.data(), 8,
+             stream);
+        EXPECT(wgot == wwant, "pack of a reordered subset (stream %d)", (int)stream);
+    }
     // byte ranges [a, b) of the packed arena (the pinned ring's chunks), cut anywhere
-    for (int rep = 0; rep < 50; rep++) {
+    // (stream: non-temporal stores, destinations at every alignment)
+    for (int rep = 0; rep < 100; rep++) {
+        const bool stream = rep & 1;
         uint64_t a = rng() % (total + 1), b = rng() % (total + 1);
         if (a > b) std::swap(a, b);
-        std::vector<uint8_t> got(b - a + 1, 0x55);
-        pack_range(nullptr, ptr.data(), len.data(), first.data(), n, poff.data(), a, b, got.data(),
-                   1 + (int)(rng() % 16));
-        EXPECT(std::equal(got.begin(), got.begin() + (long)(b - a), want.begin() + (long)a),
-               "pack_range [%llu, %llu)", (unsigned long long)a, (unsigned long long)b);
+        const uint64_t skew = rng() % 16;
+        std::vector<uint8_t> buf_got(b - a + 1 + skew, 0x55);
+        uint8_t* got = buf_got.data() + skew;
+        pack_range(nullptr, ptr.data(), len.data(), first.data(), n, poff.data(), a, b, got, 1 + (int)(rng() % 16),
+                   stream);
+        EXPECT(std::equal(got, got + (b - a), want.begin() + (long)a), "pack_range [%llu, %llu) stream %d",
+               (unsigned long long)a, (unsigned long long)b, (int)stream);
         EXPECT(got[b - a] == 0x55, "pack_range wrote past its end");
-        std::vector<uint8_t> flat(b - a + 1, 0x55);
-        pack_range(want.data(), nullptr, nullptr, nullptr, 0, nullptr, a, b, flat.data(), 1 + (int)(rng() % 16));
-        EXPECT(std::equal(flat.begin(), flat.begin() + (long)(b - a), want.begin() + (long)a),
-               "pack_range from a contiguous base");
+        std::vector<uint8_t> buf_flat(b - a + 1 + skew, 0x55);
+        uint8_t* flat = buf_flat.data() + skew;
+        pack_range(want.data(), nullptr, nullptr, nullptr, 0, nullptr, a, b, flat, 1 + (int)(rng() % 16), stream);
+        EXPECT(std::equal(flat, flat + (b - a), want.begin() + (long)a), "pack_range from a contiguous base (stream %d)",
+               (int)stream);
+        EXPECT(flat[b - a] == 0x55, "pack_range (contiguous) wrote past its end");
     }
 }
 

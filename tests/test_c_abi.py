@@ -55,20 +55,23 @@ def test_cgo_path_compiles_and_links(tmp_path):
 
 
 @pytest.mark.gpu
-def test_cgo_path_on_gpu(tmp_path):
+@pytest.mark.parametrize("stores", ["plain", "nt"])
+def test_cgo_path_on_gpu(tmp_path, stores):
     """The binding's HashBatch from C: the chunked form INTEGRATION.md now
     gives (packing of chunk k+1 overlapping chunk k's mirsha_submit_batch),
     round 4's one-call form, the serial form, the library-packed
     mirsha_hash_slices and the multi-device twin (mirsha_submit_arena_multi,
     device 0 twice): every leg agrees with the serial one (checked in the
     program) and the digests are the oracle's.  A 1 MiB chunk budget gives 27
-    chunks, far more than the 4-slot ring."""
+    chunks, far more than the 4-slot ring.  stores "nt": the workers stream
+    the arena with non-temporal stores through a per-worker window."""
     exe = build(tmp_path, PATH_SRC, "cgo_path")
     n, data_len = 100_003, 256
-    r = subprocess.run([exe, str(n), str(data_len), "8", "2", "1"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([exe, str(n), str(data_len), "8", "2", "1", stores], capture_output=True, text=True,
+                       timeout=120)
     assert r.returncode == 0, r.stderr
     line = json.loads(r.stdout.splitlines()[-1])
-    assert line["requests"] == n and line["parallel"]["ms"] > 0
+    assert line["requests"] == n and line["parallel"]["ms"] > 0 and line["pack_stores"] == stores
     # requests per chunk (a chunk ends at a request boundary; the first has a quarter of the budget)
     per, first = -(-(1 << 20) // (16 + data_len)), -(-(1 << 18) // (16 + data_len))
     assert line["parallel"]["chunks"] == 1 + -(-(n - first) // per) == line["multi"]["chunks"] == 27
