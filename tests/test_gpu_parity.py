@@ -133,6 +133,23 @@ def test_large_single_message(eng):
     assert eng.hash_messages([m])[0].tobytes() == hashlib.sha256(m).digest()
 
 
+def test_messages_past_2_pow_29_bytes(engine):
+    """Bit lengths of 2^32 and more: the length block's high word (L >> 29)
+    is nonzero only for messages of 512 MiB and up.  Two such messages (high
+    word 1 with a zero low word, and with a nonzero one) beside short ones in
+    one call; each is an 8.4 M-compression chain in one lane (~15-20 s)."""
+    rng = np.random.default_rng(29)
+    lens = [100, 1 << 29, 55, (1 << 29) + 4097, 0]
+    arena = np.frombuffer(rng.bytes(sum(lens)), dtype=np.uint8)
+    off = np.zeros(len(lens), dtype=np.uint64)
+    np.cumsum(np.array(lens[:-1], dtype=np.uint64), out=off[1:])
+    got = engine.hash_batch(arena, off, np.array(lens, dtype=np.uint32))
+    mv = memoryview(arena)
+    for i, L in enumerate(lens):
+        o = int(off[i])
+        assert got[i].tobytes() == hashlib.sha256(mv[o:o + L]).digest(), f"message {i} ({L} bytes)"
+
+
 def test_testengine_requests(eng, layouts):
     rs = layouts["testengine_requests"]
     reqs = [hashdata.request_hash_data(r["client"], r["req_no"],
