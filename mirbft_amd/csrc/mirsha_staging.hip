@@ -202,21 +202,22 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     };
     const uint64_t total = src.total;
     const uint32_t entries = n_lists ? first[n_lists] : 0u;
-    // Chunk k covers arena bytes [cb[k], cb[k+1]).
+    // Chunk k covers arena bytes [cb[k], cb[k+1]): 8, 16, then 32 MiB, so the
+    // link is busy early while the pool fills the next (larger) chunk.
     std::vector<uint64_t> cb{0};
-    for (uint64_t x = std::min(total, kFirstChunk); ; x = std::min(total, x + kStageChunk)) {
+    for (uint64_t x = 0, step = kFirstChunk; x < total; step = std::min(2 * step, kStageChunk)) {
+        x = std::min(total, x + step);
         cb.push_back(x);
-        if (x == total) break;
     }
     const uint32_t nch = (uint32_t)cb.size() - 1;
     if (!c->xin) HIP_TRY(c, hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
     if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
-    // events: in[k], kern[k], out[k] per chunk; meta; lists kernel; lists out
-    HIP_TRY(c, take_events(c, 3ull * nch + 3));
+    // events: in[k], kern[k], out[k] per chunk; lists kernel; lists out
+    HIP_TRY(c, take_events(c, 3ull * nch + 2));
     hipEvent_t* ev_in = c->xev.data();
     hipEvent_t* ev_kern = ev_in + nch;
     hipEvent_t* ev_out = ev_kern + nch;
-    hipEvent_t ev_meta = ev_out[nch], ev_lk = ev_out[nch + 1], ev_lo = ev_out[nch + 2];
+    hipEvent_t ev_lk = ev_out[nch], ev_lo = ev_out[nch + 1];
     HIP_TRY(c, c->d_arena.ensure(total + kArenaSlack));
     uint8_t* d_arena = c->d_arena.as<uint8_t>();
     const bool pinned_src = src.base && host_pinned(src.base);
@@ -241,10 +242,20 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         mark("in", k);
         return MIRSHA_OK;
     };
-    if (int rc = queue_in(0)) return rc;
+    // Before the plan: every chunk of a page-locked arena (DMA queued only),
+    // else as many as the ring holds, so the plan's host time runs under
+    // their DMA instead of leaving the link idle.
+    uint32_t queued = 0;
+    auto queue_upto = [&](uint32_t m) -> int {
+        for (; queued < m; queued++)
+            if (int rc = queue_in(queued)) return rc;
+        return MIRSHA_OK;
+    };
+    if (int rc = queue_upto(pinned_src ? nch : std::min<uint32_t>(nch, (uint32_t)kStageSlots))) return rc;
 
-    // Metadata (behind chunk 0 on the same copy stream).  Chunk k hashes the
-    // messages [cut[k], cut[k+1]): those ending within its bytes [0, cb[k+1]).
+    // Metadata, on the kernel stream (not behind the chunks on xin).  Chunk k
+    // hashes the messages [cut[k], cut[k+1]): those ending within its bytes
+    // [0, cb[k+1]).
     const auto tp = Clock::now();
     std::vector<uint32_t> cut(nch + 1, 0);
     for (uint32_t k = 0; k + 1 < nch; k++) {
@@ -260,8 +271,10 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     // Lengths first (and whether the block counts differ), then the layout.
     HIP_TRY(c, c->h_meta.ensure(PipeLayout(n, entries, n_lists, true, false).end));
     uint8_t* h = c->h_meta.as<uint8_t>();
+    // (The plan's passes run while the first chunks cross PCIe: spread wide,
+    // ~32 bytes of work per request.)
     std::atomic<uint32_t> lo_b{UINT32_MAX}, hi_b{0};
-    mirsha::host::parallel_for(n, mirsha::host::threads_for(4ull * n, n), [&](uint32_t a, uint32_t b) {
+    mirsha::host::parallel_for(n, mirsha::host::threads_for(32ull * n, n), [&](uint32_t a, uint32_t b) {
         uint32_t* hl = reinterpret_cast<uint32_t*>(h);
         uint32_t lo = UINT32_MAX, hi = 0;
         for (uint32_t i = a; i < b; i++) {
@@ -280,7 +293,7 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     HIP_TRY(c, c->d_meta.ensure(L.end));
     if (!gapless) {
         uint64_t* ho = reinterpret_cast<uint64_t*>(h + L.off);
-        mirsha::host::parallel_for(n, mirsha::host::threads_for(8ull * n, n), [&](uint32_t a, uint32_t b) {
+        mirsha::host::parallel_for(n, mirsha::host::threads_for(32ull * n, n), [&](uint32_t a, uint32_t b) {
             for (uint32_t i = a; i < b; i++) ho[i] = off[i] - shift;
         });
     }
@@ -292,9 +305,7 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     }
     if (entries) pmemcpy(h + L.idx, idx, 4ull * entries);
     if (n_lists) pmemcpy(h + L.first, first, 4ull * (n_lists + 1));
-    HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.copy, hipMemcpyHostToDevice, c->xin));
-    HIP_TRY(c, hipEventRecord(ev_meta, c->xin));
-    HIP_TRY(c, hipStreamWaitEvent(c->stream, ev_meta, 0));
+    HIP_TRY(c, hipMemcpyAsync(c->d_meta.p, h, L.copy, hipMemcpyHostToDevice, c->stream));
     uint8_t* dm = c->d_meta.as<uint8_t>();
     if (gapless) {  // off = exclusive scan of len, on the device
         size_t tb = 0;
@@ -326,8 +337,7 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         }
     };
     for (uint32_t k = 0; k < nch; k++) {
-        if (k > 0)
-            if (int rc = queue_in(k)) return rc;
+        if (int rc = queue_upto(k + 1)) return rc;
         const uint32_t i0 = cut[k], cnt = cut[k + 1] - i0;
         HIP_TRY(c, hipStreamWaitEvent(c->stream, ev_in[k], 0));
         if (cnt) {
@@ -370,22 +380,25 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
         HIP_TRY(c, hipMemcpyAsync(h_lst, d_lst, 32ull * n_lists, hipMemcpyDeviceToHost, c->xout));
         HIP_TRY(c, hipEventRecord(ev_lo, c->xout));
     }
-    // The rest: all but the last chunk are usually back by now (one copy for
-    // them), then the last chunk and the lists.
-    if (copied + 1 < nch) {
+    // The rest as it comes back: wait for the next chunk, copy it together
+    // with every later chunk already back, while the remaining DMA runs.
+    while (copied < nch) {
         const auto w = Clock::now();
-        HIP_TRY(c, hipEventSynchronize(ev_out[nch - 2]));
+        HIP_TRY(c, hipEventSynchronize(ev_out[copied]));
         t_wait += ms_since(w);
-        mark("w", nch - 2);
-        copy_out(copied, nch - 1);
-        copied = nch - 1;
-    }
-    if (copied < nch) {
-        const auto w = Clock::now();
-        HIP_TRY(c, hipEventSynchronize(ev_out[nch - 1]));
-        t_wait += ms_since(w);
-        mark("w", nch - 1);
-        copy_out(copied, nch);
+        mark("w", copied);
+        uint32_t ready = copied + 1;
+        while (ready < nch) {
+            const hipError_t q = hipEventQuery(ev_out[ready]);
+            if (q == hipErrorNotReady) {
+                (void)hipGetLastError();
+                break;
+            }
+            if (q != hipSuccess) return fail(c, MIRSHA_EHIP, "hipEventQuery: %s", hipGetErrorString(q));
+            ready++;
+        }
+        copy_out(copied, ready);
+        copied = ready;
     }
     if (n_lists) {
         const auto w = Clock::now();
