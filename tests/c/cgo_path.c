@@ -354,8 +354,16 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
     int nk = 0;
     for (uint32_t lo = 0; lo < n;) {
         const uint64_t budget = nk ? chunk_bytes : chunk_bytes / 4;
-        uint32_t hi = lo + 1;
-        while (hi < n && off[hi] - off[lo] < budget) hi++;
+        /* hi = the first index past lo with off[hi] - off[lo] >= budget, else n
+         * (binary search: off is nondecreasing) */
+        uint32_t hi = lo + 1, top = n;
+        while (hi < top) {
+            const uint32_t mid = hi + (top - hi) / 2;
+            if (off[mid] - off[lo] < budget)
+                hi = mid + 1;
+            else
+                top = mid;
+        }
         if (nk == MAX_CHUNKS) exit(6);
         cfirst[nk++] = lo;
         lo = hi;
