@@ -350,10 +350,12 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
     ph_off = now_ms() - t0;
     ph_pack = ph_submit = 0.0;
     /* chunk boundaries: requests [lo, hi) until the chunk's bytes reach the
-     * budget (a quarter of it for the first chunk, so the DMA starts early) */
+     * budget */
     int nk = 0;
     for (uint32_t lo = 0; lo < n;) {
-        const uint64_t budget = nk ? chunk_bytes : chunk_bytes / 4;
+        /* a quarter, a half, then whole budgets: the link starts early and
+         * stays busy while the workers pack the next, larger chunk */
+        const uint64_t budget = nk == 0 ? chunk_bytes / 4 : nk == 1 ? chunk_bytes / 2 : chunk_bytes;
         /* hi = the first index past lo with off[hi] - off[lo] >= budget, else n
          * (binary search: off is nondecreasing) */
         uint32_t hi = lo + 1, top = n;

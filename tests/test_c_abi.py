@@ -62,7 +62,7 @@ def test_cgo_path_on_gpu(tmp_path, stores):
     round 4's one-call form, the serial form, the library-packed
     mirsha_hash_slices and the multi-device twin (mirsha_submit_arena_multi,
     device 0 twice): every leg agrees with the serial one (checked in the
-    program) and the digests are the oracle's.  A 1 MiB chunk budget gives 27
+    program) and the digests are the oracle's.  A 1 MiB chunk budget gives 28
     chunks, far more than the 4-slot ring.  stores "nt": the workers stream
     the arena with non-temporal stores through a per-worker window."""
     exe = build(tmp_path, PATH_SRC, "cgo_path")
@@ -72,9 +72,10 @@ def test_cgo_path_on_gpu(tmp_path, stores):
     assert r.returncode == 0, r.stderr
     line = json.loads(r.stdout.splitlines()[-1])
     assert line["requests"] == n and line["parallel"]["ms"] > 0 and line["pack_stores"] == stores
-    # requests per chunk (a chunk ends at a request boundary; the first has a quarter of the budget)
-    per, first = -(-(1 << 20) // (16 + data_len)), -(-(1 << 18) // (16 + data_len))
-    assert line["parallel"]["chunks"] == 1 + -(-(n - first) // per) == line["multi"]["chunks"] == 27
+    # requests per chunk (a chunk ends at a request boundary; the first two
+    # have a quarter and a half of the budget)
+    per, first, second = (-(-(1 << b) // (16 + data_len)) for b in (20, 18, 19))
+    assert line["parallel"]["chunks"] == 2 + -(-(n - first - second) // per) == line["multi"]["chunks"] == 28
     arena = oracle_py.gen_requests(0x6D69726266740002, 0, 4, data_len)
     stride = 16 + data_len
     want = oracle_py.hash_requests(arena, np.arange(4, dtype=np.uint64) * stride, np.full(4, stride))

@@ -55,6 +55,31 @@ int main() {
         first = false;
         fflush(stdout);
     }
+    // D2H of digest-sized copies (a 32 MiB chunk of config 2 returns 3.9 MB),
+    // alone and while a 32 MiB H2D runs on another stream.
+    hipStream_t s2;
+    (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (size_t sz : {1ull << 20, 4ull << 20, 16ull << 20, 64ull << 20})
+        for (int busy = 0; busy < 2; busy++) {
+            std::vector<double> t;
+            for (int r = 0; r < 10; r++) {
+                if (busy) (void)hipMemcpyAsync(d, h, chunk, hipMemcpyHostToDevice, s2);
+                (void)hipEventRecord(e0, s);
+                (void)hipMemcpyAsync((char*)h + chunk, (const char*)d + chunk, sz, hipMemcpyDeviceToHost, s);
+                (void)hipEventRecord(e1, s);
+                (void)hipStreamSynchronize(s);
+                (void)hipStreamSynchronize(s2);
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, e0, e1);
+                if (r) t.push_back(ms * 1e-3);
+            }
+            std::sort(t.begin(), t.end());
+            printf(", \"d2h_%zuMiB%s_gbs\": %.1f", sz >> 20, busy ? "_during_h2d" : "", sz / t[t.size() / 2] / 1e9);
+            fflush(stdout);
+        }
     printf("}\n");
     (void)hipHostFree(h);
     (void)hipFree(d);
