@@ -96,6 +96,21 @@ int d2h_split(mirsha_ctx* c, const uint8_t* d_src, uint64_t total, uint64_t spli
     return MIRSHA_OK;
 }
 
+// A synchronous call that fails after queueing copies returns only once the
+// context's streams have drained: nothing may still read the caller's arena
+// or write its outputs after the call returns.  Disarmed on success (every
+// queued operation was waited for).
+struct DrainOnError {
+    mirsha_ctx* c;
+    bool on = true;
+    ~DrainOnError() {
+        if (!on) return;
+        (void)hipStreamSynchronize(c->stream);
+        if (c->xin) (void)hipStreamSynchronize(c->xin);
+        if (c->xout) (void)hipStreamSynchronize(c->xout);
+    }
+};
+
 // Layout of the per-call metadata block (pinned and on device).
 struct MetaLayout {
     uint64_t off, len, order, idx, first, arena, end;
@@ -212,6 +227,9 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     const uint32_t nch = (uint32_t)cb.size() - 1;
     if (!c->xin) HIP_TRY(c, hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
     if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
+    // A failure after the first copy is queued returns only once the streams
+    // have drained (DrainOnError).
+    DrainOnError drain{c};
     // events: in[k], kern[k], out[k] per chunk; lists kernel; lists out
     HIP_TRY(c, take_events(c, 3ull * nch + 2));
     hipEvent_t* ev_in = c->xev.data();
@@ -413,6 +431,7 @@ int run_pipelined(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const
     c->prof[MIRSHA_PROF_DEVICE] = t_wait;
     c->prof[MIRSHA_PROF_SCATTER] = t_out;
     c->prof[MIRSHA_PROF_CHUNKS] = nch;
+    drain.on = false;  // every event waited for above
     return MIRSHA_OK;
 }
 
@@ -454,6 +473,7 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
     const bool inl = src.total <= kInlineArena;
     // Large arenas first: their chunks DMA while the metadata is built.
     HIP_TRY(c, c->d_arena.ensure(inl ? 1 : src.total + kArenaSlack));
+    DrainOnError drain{c};
     if (!inl)
         if (int rc = h2d_arena(c, src, c->d_arena.as<uint8_t>())) return rc;
     c->prof[MIRSHA_PROF_PACK] = ms_since(t0);
@@ -521,6 +541,7 @@ int run_staged(mirsha_ctx* c, const ArenaSrc& src, const uint64_t* off, const ui
     }
     c->prof[MIRSHA_PROF_SCATTER] = ms_since(t0);
     for (bool& b : c->ring_busy) b = false;  // every queued chunk DMA has completed
+    drain.on = false;
     return MIRSHA_OK;
 }
 
