@@ -51,15 +51,20 @@ constexpr uint32_t kFusedMinChainBlocks = 64;    // AUTO picks the fused launch 
 constexpr uint32_t kFusedDefaultPace = 4;        // tile waves (= tile queues) per SIMD
 constexpr uint32_t kFusedDefaultListTiles = 1;   // FusedArgs::list_tiles (fused_build; profiles/r02au, r02av)
 
+// Grow-only buffers.  A growth frees (hipFree / hipHostFree synchronise the
+// device: every queued copy and kernel of every stream must finish first),
+// so a buffer grows to 1.5x its old capacity, not to the exact request: ring
+// slots see chunks a few hundred bytes apart, and exact-fit growth cost a
+// ~9 ms device drain inside a submission now and then (profiles/r05w).
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
+        size_t want = std::max(n, cap + cap / 2);
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t want = std::max(n, cap + cap / 2);
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) {
             (void)hipGetLastError();
@@ -79,12 +84,18 @@ struct PinnedBuf {
     size_t cap = 0;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
+        size_t want = std::max(n, cap + cap / 2);
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
-        if (e != hipSuccess) { p = nullptr; return e; }
-        cap = n;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            e = hipHostMalloc(&p, n, hipHostMallocDefault);
+            if (e != hipSuccess) { p = nullptr; return e; }
+            want = n;
+        }
+        cap = want;
         return hipSuccess;
     }
     template <class T> T* as() const { return static_cast<T*>(p); }

@@ -332,6 +332,9 @@ static void hash_batch_onecall(const Request* reqs, uint32_t n, uint8_t* arena, 
 /* host phases of the last chunked call (ms): offsets, waiting for the packing
  * workers, submits (overlapping the packing), final wait, final copy */
 static double ph_off, ph_pack, ph_submit, ph_wait, ph_copy;
+/* the longest single submit and the longest wait for the workers in one call:
+ * a host that deschedules a worker shows up in the latter */
+static double ph_max_submit, ph_max_pool;
 static void submit_chunk(mirsha_multi* m, const uint8_t* arena, uint64_t total, const uint64_t* off,
                          const uint32_t* lens, uint32_t lo, uint32_t hi, uint8_t* dig_pinned, uint64_t* ticket) {
     if (m)
@@ -348,7 +351,7 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
     const double t0 = now_ms();
     const uint64_t total = offsets_parallel(reqs, n, off, lens, pool);
     ph_off = now_ms() - t0;
-    ph_pack = ph_submit = 0.0;
+    ph_pack = ph_submit = ph_max_submit = ph_max_pool = 0.0;
     /* chunk boundaries: requests [lo, hi) until the chunk's bytes reach the
      * budget */
     int nk = 0;
@@ -398,8 +401,11 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
         if (k > 0) submit_chunk(m, arena, total, off, lens, cfirst[k - 1], cfirst[k], dig_pinned, &ticket[k - 1]);
         const double tw = now_ms();
         ph_submit += tw - ts;
+        if (tw - ts > ph_max_submit) ph_max_submit = tw - ts;
         if (k < nk || job.dhi > job.dlo) pool_wait(pool);
-        ph_pack += (ts - tp) + (now_ms() - tw);
+        const double te = now_ms();
+        ph_pack += (ts - tp) + (te - tw);
+        if (te - tw > ph_max_pool) ph_max_pool = te - tw;
     }
     const double t1 = now_ms();
     if (nk) {
@@ -511,6 +517,7 @@ int main(int argc, char** argv) {
 
     Leg ser, par, one, lib, mul;
     char phases[512] = "";
+    char calls[64 * 96 + 32] = ", \"calls\": [";
     int chunks = 0, mchunks = 0;
     for (int r = -1; r < reps; r++) { /* r = -1: warm-up */
         double a, b;
@@ -518,6 +525,12 @@ int main(int argc, char** argv) {
         leg_put(&ser, r, a, b);
         hash_batch_chunked(reqs, n, arena, off, lens, dig_pinned, dig_p, &pool, chunk_bytes, NULL, &a, &b, &chunks);
         leg_put(&par, r, a, b);
+        if (r >= 0) {
+            char one_call[96];
+            snprintf(one_call, sizeof one_call, "%s[%.2f, %.2f, %.2f, %.2f]", r ? ", " : "", a + b, ph_max_pool,
+                     ph_max_submit, ph_wait);
+            strcat(calls, one_call);
+        }
         if (r == reps - 1) {
             /* the library's phases of the last chunk's submission (validate, plan, queue) */
             double lp[MIRSHA_PROF_PHASES] = {0};
@@ -578,9 +591,10 @@ int main(int argc, char** argv) {
         fprintf(stderr, "legs disagree\n");
         return 1;
     }
-    char sample[4 * 65 + 8], extra[640], mextra[96];
+    char sample[4 * 65 + 8], extra[8192], mextra[96];
     hex4(dig_s, sample);
-    snprintf(extra, sizeof extra, ", \"chunks\": %d, \"chunk_mib\": %.2f%s", chunks, chunk_mib, phases);
+    strcat(calls, "], \"calls_note\": \"per call: ms, longest wait for the workers, longest submit, final wait\"");
+    snprintf(extra, sizeof extra, ", \"chunks\": %d, \"chunk_mib\": %.2f%s%s", chunks, chunk_mib, phases, calls);
     snprintf(mextra, sizeof mextra, ", \"chunks\": %d, \"devices\": %d", mchunks, nd);
     printf("{\"requests\": %u, \"request_bytes\": %u, \"bytes\": %llu, \"threads\": %d, \"reps\": %d, "
            "\"pack_stores\": \"%s\", ",
