@@ -193,7 +193,21 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
 int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
                        const uint32_t* len, uint32_t n, uint8_t* out, uint64_t* ticket_out) {
     auto t0 = Clock::now();
+    const auto t_entry = t0;
     double ph[MIRSHA_PROF_PHASES] = {};
+    // MIRSHA_SUBMIT_TRACE=1 (with MIRSHA_AB=1): a submission slower than 2 ms
+    // prints where its time went (ms since entry at each step) on stderr.
+    double tr[6] = {}, tq[8] = {};
+    auto trace_done = [&](const char* how) {
+        const double tot = ms_since(t_entry);
+        if (tot > 2.0 && getenv_flag("MIRSHA_SUBMIT_TRACE"))
+            fprintf(stderr,
+                    "mirsha submit trace: %.3f ms (%s): slot wait %.3f, meta buffer %.3f, validate %.3f, "
+                    "buffers %.3f, pack %.3f, queue %.3f [ev_in %.3f meta %.3f wait %.3f scan %.3f kernel %.3f "
+                    "ev_kern %.3f d2h %.3f done %.3f]\n",
+                    tot, how, tr[0], tr[1], tr[2], tr[3], tr[4], tr[5], tq[0], tq[1], tq[2], tq[3], tq[4], tq[5],
+                    tq[6], tq[7]);
+    };
     // One pass over the n entries on the calling thread (up to 2^18
     // requests: a chunk of the Go binding's HashBatch is ~120k requests and
     // its goroutines pack the NEXT chunk meanwhile): bounds, the span [lo,
@@ -220,8 +234,10 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     AsyncSlot& sl = c->slots[(c->next_ticket - 1) % kAsyncSlots];
     if (sl.busy)
         if (int rc = async_wait_upto(c, sl.ticket)) return rc;  // ring full: retire the oldest
+    tr[0] = ms_since(t_entry);
     const uint64_t o_len = 0, o_ord = align8(4ull * n), o_off = align8(o_ord + 4ull * n), o_end = o_off + 8ull * n;
     HIP_TRY(c, sl.stage2.ensure(std::max<uint64_t>(o_end, 8)));
+    tr[1] = ms_since(t_entry);
     uint8_t* mb = sl.stage2.as<uint8_t>();
     uint32_t* slen = reinterpret_cast<uint32_t*>(mb + o_len);
     uint32_t* sord = reinterpret_cast<uint32_t*>(mb + o_ord);
@@ -291,6 +307,7 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     // bytes of the metadata block that cross PCIe
     const uint64_t meta_copy = !gapless ? o_end : !identity ? o_ord + 4ull * n : 4ull * n;
     ph[MIRSHA_PROF_VALIDATE] = ms_since(t0);
+    tr[2] = ms_since(t_entry);
     t0 = Clock::now();
     sl.rank.clear();
     for (hipEvent_t* e : {&sl.done, &sl.ev_in, &sl.ev_kern})
@@ -315,6 +332,7 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     HIP_TRY(c, sl.dev.ensure(d_dig + 32ull * n));
     uint8_t* st = sl.stage.as<uint8_t>();
     ph[MIRSHA_PROF_PLAN] = ms_since(t0);
+    tr[3] = ms_since(t_entry);
     t0 = Clock::now();
     uint8_t* dv = sl.dev.as<uint8_t>();
     if (from_caller) {
@@ -335,6 +353,7 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         mirsha::host::pack(sp.data(), sz.data(), sf.data(), nullptr, n, soff, st, mirsha::host::threads_for(bytes, n),
                            true);
     }
+    tr[4] = ms_since(t_entry);
     // Queue the copies and the kernel.  A failure part-way leaves work that
     // reads this slot's buffers in flight while the slot is not marked busy:
     // drain the three streams before reporting it.
@@ -342,15 +361,19 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         if (n) {
             if (!from_caller && bytes) HIP_TRY(c, hipMemcpyAsync(dv, st, bytes, hipMemcpyHostToDevice, c->xin));
             HIP_TRY(c, hipEventRecord(sl.ev_in, c->xin));
+            tq[0] = ms_since(t_entry);
             // The metadata on the kernel stream: xin carries only request
             // bytes, back to back across submissions (a small copy between
             // two chunks on xin cost ~30 us of link time, profiles/r05t).
             HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, meta_copy, hipMemcpyHostToDevice, c->stream));
+            tq[1] = ms_since(t_entry);
             HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.ev_in, 0));
+            tq[2] = ms_since(t_entry);
             uint64_t* d_off = reinterpret_cast<uint64_t*>(dv + d_meta + o_off);
             const uint32_t* d_len = reinterpret_cast<const uint32_t*>(dv + d_meta + o_len);
             if (gapless)  // off = exclusive scan of len, on the device (c->d_scan: c->stream's scratch)
                 HIP_TRY(c, mirsha::launch_offsets_scan(c->d_scan.p, scan_bytes, d_len, d_off, n, c->stream));
+            tq[3] = ms_since(t_entry);
             if (int rc = timed_launch(c, 0, [&] {
                     return mirsha::launch_msgs(dv, bytes, d_off, d_len,
                                                identity ? nullptr
@@ -358,12 +381,16 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
                                                n, dv + d_dig, c->variant, c->stream);
                 }))
                 return rc;
+            tq[4] = ms_since(t_entry);
             HIP_TRY(c, hipEventRecord(sl.ev_kern, c->stream));
             HIP_TRY(c, hipStreamWaitEvent(c->xout, sl.ev_kern, 0));
+            tq[5] = ms_since(t_entry);
             HIP_TRY(c, hipMemcpyAsync(sl.direct ? out : sl.dig.as<uint8_t>(), dv + d_dig, 32ull * n,
                                       hipMemcpyDeviceToHost, c->xout));
+            tq[6] = ms_since(t_entry);
         }
         HIP_TRY(c, hipEventRecord(sl.done, c->xout));
+        tq[7] = ms_since(t_entry);
         return MIRSHA_OK;
     };
     if (int rc = queue()) {
@@ -372,6 +399,8 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     }
     sl.t_queued = Clock::now();
     ph[MIRSHA_PROF_PACK] = ms_since(t0);
+    tr[5] = ms_since(t_entry);
+    trace_done("arena");
     sl.busy = true;
     sl.user_out = out;
     sl.n = n;

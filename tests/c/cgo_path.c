@@ -8,7 +8,9 @@
  * every slice its own heap allocation, as Go's [][]byte slices are.  A
  * persistent pool of `threads` workers stands in for GOMAXPROCS goroutines
  * (a goroutine start costs ~1 us; a pthread_create per chunk would not).
- * Legs, each the median of `reps` calls after one warm-up:
+ * Legs, each the median of `reps` calls after three warm-up calls (a fresh
+ * process's first few calls can block ~9 ms in an SDMA copy enqueue of the
+ * HIP runtime, profiles/r05w; a consensus node calls HashBatch every cycle):
  *   serial    round 2's HashBatch: one goroutine packs every slice into the
  *             mirsha_host_alloc arena, then one mirsha_hash_batch;
  *   parallel  INTEGRATION.md's HashBatch: offsets first, then the cycle in
@@ -335,6 +337,9 @@ static double ph_off, ph_pack, ph_submit, ph_wait, ph_copy;
 /* the longest single submit and the longest wait for the workers in one call:
  * a host that deschedules a worker shows up in the latter */
 static double ph_max_submit, ph_max_pool;
+/* the library's phases of the slowest submit seen (> 3 ms): where it blocked */
+static double slow_submit[MIRSHA_PROF_PHASES];
+static double slow_submit_ms;
 static void submit_chunk(mirsha_multi* m, const uint8_t* arena, uint64_t total, const uint64_t* off,
                          const uint32_t* lens, uint32_t lo, uint32_t hi, uint8_t* dig_pinned, uint64_t* ticket) {
     if (m)
@@ -402,6 +407,10 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
         const double tw = now_ms();
         ph_submit += tw - ts;
         if (tw - ts > ph_max_submit) ph_max_submit = tw - ts;
+        if (!m && k > 0 && tw - ts > 3.0 && tw - ts > slow_submit_ms) {
+            slow_submit_ms = tw - ts;
+            mirsha_ctx_host_profile(ctx, slow_submit, MIRSHA_PROF_PHASES);
+        }
         if (k < nk || job.dhi > job.dlo) pool_wait(pool);
         const double te = now_ms();
         ph_pack += (ts - tp) + (te - tw);
@@ -459,6 +468,8 @@ static void leg_print(const char* name, Leg* l, int reps, uint32_t n, const char
     printf("\"%s\": {\"pack_ms\": %.3f, \"call_ms\": %.3f, \"ms\": %.3f, \"digests_per_s\": %.1f%s}", name,
            median(l->pack, reps), median(l->call, reps), t, n / (t * 1e-3), extra);
 }
+
+enum { kWarm = 3 }; /* untimed calls per leg before the timed ones */
 
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? (uint32_t)strtoul(argv[1], NULL, 10) : (1u << 20);
@@ -519,7 +530,7 @@ int main(int argc, char** argv) {
     char phases[512] = "";
     char calls[64 * 96 + 32] = ", \"calls\": [";
     int chunks = 0, mchunks = 0;
-    for (int r = -1; r < reps; r++) { /* r = -1: warm-up */
+    for (int r = -kWarm; r < reps; r++) { /* r < 0: warm-up */
         double a, b;
         hash_batch_onecall(reqs, n, arena, off, lens, dig_s, NULL, &a, &b);
         leg_put(&ser, r, a, b);
@@ -557,7 +568,7 @@ int main(int argc, char** argv) {
         sf[i] = 3u * i;
     }
     sf[n] = 3u * n;
-    for (int r = -1; r < reps; r++) {
+    for (int r = -kWarm; r < reps; r++) {
         const double t0 = now_ms();
         CHECK(mirsha_hash_slices(ctx, sp, sl, sf, n, dig_l));
         leg_put(&lib, r, 0.0, now_ms() - t0);
@@ -581,7 +592,7 @@ int main(int argc, char** argv) {
     CHECK(mirsha_multi_create(devs, nd, &multi));
     CHECK(mirsha_multi_host_alloc(multi, total + 1, &ap));
     CHECK(mirsha_multi_host_alloc(multi, 32ull * n, &dp));
-    for (int r = -1; r < reps; r++) {
+    for (int r = -kWarm; r < reps; r++) {
         double a, b;
         hash_batch_chunked(reqs, n, ap, off, lens, dp, dig_m, &pool, chunk_bytes, multi, &a, &b, &mchunks);
         leg_put(&mul, r, a, b);
@@ -594,6 +605,14 @@ int main(int argc, char** argv) {
     char sample[4 * 65 + 8], extra[8192], mextra[96];
     hex4(dig_s, sample);
     strcat(calls, "], \"calls_note\": \"per call: ms, longest wait for the workers, longest submit, final wait\"");
+    if (slow_submit_ms > 0) {
+        char sl[256];
+        snprintf(sl, sizeof sl,
+                 ", \"slowest_submit_ms\": {\"total\": %.3f, \"validate\": %.3f, \"plan\": %.3f, \"queue\": %.3f}",
+                 slow_submit_ms, slow_submit[MIRSHA_PROF_VALIDATE], slow_submit[MIRSHA_PROF_PLAN],
+                 slow_submit[MIRSHA_PROF_PACK]);
+        strcat(calls, sl);
+    }
     snprintf(extra, sizeof extra, ", \"chunks\": %d, \"chunk_mib\": %.2f%s%s", chunks, chunk_mib, phases, calls);
     snprintf(mextra, sizeof mextra, ", \"chunks\": %d, \"devices\": %d", mchunks, nd);
     printf("{\"requests\": %u, \"request_bytes\": %u, \"bytes\": %llu, \"threads\": %d, \"reps\": %d, "
