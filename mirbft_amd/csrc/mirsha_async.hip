@@ -312,14 +312,29 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     sl.rank.clear();
     for (hipEvent_t* e : {&sl.done, &sl.ev_in, &sl.ev_kern})
         if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
-    // Three streams, as the pipelined synchronous calls: request bytes in on
-    // xin, metadata and the kernel on the context stream, digests out on
-    // xout.  Submission k+1's DMA runs behind submission k's DMA, not behind
+    // Request bytes in on xin, the kernel on the context stream; digests
+    // stored by the kernel into a page-locked digests_out (metadata then on
+    // xin too), else out on xout with the metadata on the kernel stream.  Submission k+1's DMA runs behind submission k's DMA, not behind
     // its kernel and D2H (PCIe is full duplex).
     if (!c->xin) HIP_TRY(c, hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
     if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
     const bool from_caller = dense && n && host_pinned(arena + lo);
     sl.direct = host_pinned(out);
+    // A page-locked digests_out is written by the kernel itself (posted
+    // writes over PCIe; visible when the kernel's completion is), and the
+    // metadata follows the request bytes on xin: every SDMA copy of the
+    // submission is then on one stream.  With copies on three streams (H2D,
+    // metadata, D2H) the runtime now and then blocked a hipMemcpyAsync for
+    // 8-15 ms (profiles/r05w: 13-22 ms calls of the chunked HashBatch); with
+    // one copy stream no call stalled, at the same steady-state speed.
+    uint8_t* kout = nullptr;
+    if (sl.direct && n) {
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, out, 0) == hipSuccess)
+            kout = static_cast<uint8_t*>(dp);
+        else
+            (void)hipGetLastError();
+    }
     if (!sl.direct) HIP_TRY(c, sl.dig.ensure(32ull * std::max<uint32_t>(n, 1)));
     // device: [request bytes + slack | len u32 | order u32 | off u64 | digests]
     const uint64_t d_meta = align8(bytes + kArenaSlack), d_dig = d_meta + o_end;
@@ -360,12 +375,12 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     auto queue = [&]() -> int {
         if (n) {
             if (!from_caller && bytes) HIP_TRY(c, hipMemcpyAsync(dv, st, bytes, hipMemcpyHostToDevice, c->xin));
+            // The metadata: behind the request bytes on xin when the kernel
+            // stores the digests (one copy stream), else on the kernel stream.
+            if (kout) HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, meta_copy, hipMemcpyHostToDevice, c->xin));
             HIP_TRY(c, hipEventRecord(sl.ev_in, c->xin));
             tq[0] = ms_since(t_entry);
-            // The metadata on the kernel stream: xin carries only request
-            // bytes, back to back across submissions (a small copy between
-            // two chunks on xin cost ~30 us of link time, profiles/r05t).
-            HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, meta_copy, hipMemcpyHostToDevice, c->stream));
+            if (!kout) HIP_TRY(c, hipMemcpyAsync(dv + d_meta, mb, meta_copy, hipMemcpyHostToDevice, c->stream));
             tq[1] = ms_since(t_entry);
             HIP_TRY(c, hipStreamWaitEvent(c->stream, sl.ev_in, 0));
             tq[2] = ms_since(t_entry);
@@ -378,10 +393,15 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
                     return mirsha::launch_msgs(dv, bytes, d_off, d_len,
                                                identity ? nullptr
                                                         : reinterpret_cast<const uint32_t*>(dv + d_meta + o_ord),
-                                               n, dv + d_dig, c->variant, c->stream);
+                                               n, kout ? kout : dv + d_dig, c->variant, c->stream);
                 }))
                 return rc;
             tq[4] = ms_since(t_entry);
+            if (kout) {  // the digests are in host memory when the kernel ends
+                HIP_TRY(c, hipEventRecord(sl.done, c->stream));
+                tq[7] = ms_since(t_entry);
+                return MIRSHA_OK;
+            }
             HIP_TRY(c, hipEventRecord(sl.ev_kern, c->stream));
             HIP_TRY(c, hipStreamWaitEvent(c->xout, sl.ev_kern, 0));
             tq[5] = ms_since(t_entry);
