@@ -189,8 +189,9 @@ int mirsha_poll(mirsha_ctx* ctx, uint64_t ticket, int* done);
  *     pageable arena is copied into the context's staging before the call
  *     returns.
  *   digests_out: C memory, valid until the ticket retires (as
- *     mirsha_submit_slices).  Page-locked (mirsha_host_alloc) digests_out
- *     receives the digests by DMA with no host copy.
+ *     mirsha_submit_slices).  A page-locked (mirsha_host_alloc) digests_out
+ *     is written by the hashing kernel itself, with no copy: its rows are
+ *     final when the ticket retires (mirsha_wait / mirsha_poll).
  *   At most MIRSHA_MAX_DEVICE_ARENA_BYTES of request bytes per submission
  *   (else MIRSHA_ERANGE; submit the cycle in chunks).  Shares the ring (4 in
  *   flight) and the tickets of mirsha_submit_slices: mirsha_wait / mirsha_poll. */
