@@ -4,6 +4,7 @@
 // staging arena (whole and by byte range, as the pinned ring fills chunk by
 // chunk), parallel_for coverage, and per-(slot, threads) packing pools.
 // Prints "host unit ok"; exit 1 with a message at the first mismatch.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -104,6 +105,27 @@ static void test_pack(std::mt19937_64& rng) {
         pack(ptr.data(), len.data(), first.data(), which.data(), (uint32_t)which.size(), woff.data(), wgot.data(), 8,
              stream);
         EXPECT(wgot == wwant, "pack of a reordered subset (stream %d)", (int)stream);
+    }
+    // destinations with gaps and out of order (the streaming writer flushes
+    // its window at every discontinuity); bytes between them stay untouched
+    {
+        std::vector<uint64_t> goff(which.size());
+        uint64_t q = 0;
+        for (size_t k = which.size(); k-- > 0;) {  // later requests at lower addresses
+            q += (k * 7) % 29;                       // a gap of 0..28 bytes
+            goff[k] = q;
+            q += rlen[which[k]];
+        }
+        std::vector<uint8_t> gwant(q, 0x77);
+        for (size_t k = 0; k < which.size(); k++)
+            std::copy(want.begin() + (long)poff[which[k]], want.begin() + (long)(poff[which[k]] + rlen[which[k]]),
+                      gwant.begin() + (long)goff[k]);
+        for (bool stream : {false, true}) {
+            std::vector<uint8_t> ggot(q, 0x77);
+            pack(ptr.data(), len.data(), first.data(), which.data(), (uint32_t)which.size(), goff.data(), ggot.data(),
+                 5, stream);
+            EXPECT(ggot == gwant, "pack to gapped, reversed destinations (stream %d)", (int)stream);
+        }
     }
     // byte ranges [a, b) of the packed arena (the pinned ring's chunks), cut anywhere
     // (stream: non-temporal stores, destinations at every alignment)
