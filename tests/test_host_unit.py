@@ -13,13 +13,13 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _build_and_run(tmp_path, name, flags):
+def _build_and_run(tmp_path, name, flags, env=None):
     exe = str(tmp_path / name)
     subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-pthread", *flags,
                     "-I", os.path.join(ROOT, "mirbft_amd", "csrc"), "-I", os.path.join(ROOT, "include"),
                     os.path.join(ROOT, "tests", "c", "host_unit.cpp"),
                     os.path.join(ROOT, "mirbft_amd", "csrc", "mirsha_host.cpp"), "-o", exe], check=True)
-    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     assert r.stdout.strip() == "host unit ok"
 
@@ -35,4 +35,6 @@ def test_host_helpers_sanitized(tmp_path):
         pytest.skip("g++ without ASan/UBSan runtime")
     _build_and_run(tmp_path, "host_unit_asan",
                    ["-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
-                    "-fno-omit-frame-pointer"])
+                    "-fno-omit-frame-pointer"],
+                   # a preloaded library (some sandboxes add one) must not stop ASan at startup
+                   env=dict(os.environ, ASAN_OPTIONS="verify_asan_link_order=0"))
