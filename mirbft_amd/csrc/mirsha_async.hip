@@ -314,8 +314,9 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
         if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
     // Request bytes in on xin, the kernel on the context stream; digests
     // stored by the kernel into a page-locked digests_out (metadata then on
-    // xin too), else out on xout with the metadata on the kernel stream.  Submission k+1's DMA runs behind submission k's DMA, not behind
-    // its kernel and D2H (PCIe is full duplex).
+    // xin too), else out on xout with the metadata on the kernel stream.
+    // Submission k+1's DMA runs behind submission k's DMA, not behind its
+    // kernel (PCIe is full duplex).
     if (!c->xin) HIP_TRY(c, hipStreamCreateWithFlags(&c->xin, hipStreamNonBlocking));
     if (!c->xout) HIP_TRY(c, hipStreamCreateWithFlags(&c->xout, hipStreamNonBlocking));
     const bool from_caller = dense && n && host_pinned(arena + lo);
