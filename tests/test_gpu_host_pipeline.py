@@ -195,3 +195,24 @@ def test_gapless_shifted_arena_device_offsets(engine, monkeypatch):
     monkeypatch.setenv("MIRSHA_AB", "1")
     monkeypatch.setenv("MIRSHA_NO_OFFSET_SCAN", "1")
     assert np.array_equal(engine.hash_batch(arena, off, lens), a)
+
+
+def test_arena_past_4gib_pipelined_and_single_shot(engine):
+    """A host arena larger than one 32-bit buffer descriptor (4 GiB): ragged
+    ~8 KB requests go through the pipelined path with every chunk's kernel in
+    the 64-bit-address form; then the same bytes as ~64 KB requests, longer
+    than the pipelined path takes, through single-shot staging."""
+    rng = np.random.default_rng(4)
+    total_min = (1 << 32) + (64 << 20)
+    ln = rng.integers(8000, 8193, total_min // 8000 + 1).astype(np.uint32)
+    ln = ln[: int(np.searchsorted(np.cumsum(ln, dtype=np.uint64), total_min)) + 1]
+    off = np.zeros(ln.size, dtype=np.uint64)
+    np.cumsum(ln[:-1], dtype=np.uint64, out=off[1:])
+    total = int(off[-1]) + int(ln[-1])
+    assert total > (1 << 32)
+    arena = np.frombuffer(rng.bytes(total), dtype=np.uint8)
+    _check(engine, arena, off, ln, min_chunks=100)
+    # ~64 KB requests: past the pipelined path's per-message limit
+    big = np.full(total // 65000, 65000, dtype=np.uint32)
+    boff = np.arange(big.size, dtype=np.uint64) * 65000
+    _check(engine, arena, boff, big)
