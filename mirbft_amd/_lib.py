@@ -21,6 +21,8 @@ MIRSHA_ENOMEM = -3
 MIRSHA_ERANGE = -4
 MIRSHA_ENODEV = -5
 MIRSHA_NULL_INDEX = 0xFFFFFFFF
+MIRSHA_MAX_MESSAGE_BYTES = 0xFFFFFF00
+MIRSHA_MAX_DEVICE_ARENA_BYTES = 0xFFFFFF00
 MIRSHA_SUBMIT_DEDUP = 1
 
 ERROR_NAMES = {

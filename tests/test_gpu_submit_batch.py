@@ -123,3 +123,26 @@ def test_errors_leave_the_ring_usable(engine):
         engine.submit_batch(src, off, lens[:-1])
     t = engine.submit_batch(src, off, lens)
     assert np.array_equal(engine.wait(t), oracle_py.hash_requests(src, off, lens))
+
+
+def test_size_limits_rejected_before_any_read(engine):
+    """MIRSHA_ERANGE for a message over MIRSHA_MAX_MESSAGE_BYTES and for a
+    submission whose bytes exceed one device arena (MIRSHA_MAX_DEVICE_ARENA_BYTES):
+    both are decided from off / len alone, so a small buffer declared as a
+    huge arena is never read; the ring stays usable."""
+    import ctypes
+
+    lib, small = engine._lib, np.zeros(64, dtype=np.uint8)
+    cases = [
+        (np.array([0], dtype=np.uint64), np.array([_lib.MIRSHA_MAX_MESSAGE_BYTES + 1], dtype=np.uint32), 1 << 33),
+        (np.array([0, 3 << 30], dtype=np.uint64), np.array([3 << 30, 3 << 30], dtype=np.uint32), 6 << 30),
+    ]
+    for off, ln, arena_len in cases:
+        out = np.empty((off.size, 32), dtype=np.uint8)
+        t = ctypes.c_uint64(0)
+        rc = lib.mirsha_submit_batch(engine.ctx, small.ctypes.data, arena_len, off.ctypes.data, ln.ctypes.data,
+                                     off.size, out.ctypes.data, ctypes.byref(t))
+        assert rc == _lib.MIRSHA_ERANGE and t.value == 0
+    src, off, lens = _cycle(32, 50)
+    t = engine.submit_batch(src, off, lens)
+    assert np.array_equal(engine.wait(t), oracle_py.hash_requests(src, off, lens))
