@@ -278,6 +278,18 @@ inline bool host_pinned(const void* p) {
     return a.type == hipMemoryTypeHost;
 }
 
+// Page-locked host memory a kernel on `device` may store into: allocated or
+// registered with that device current, or portable (every device maps it).
+// Anything else takes the D2H path.
+inline bool kernel_writable_host(const void* p, int device) {
+    hipPointerAttribute_t a;
+    if (!p || hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && (a.device == device || (a.allocationFlags & hipHostMallocPortable));
+}
+
 constexpr uint64_t align8(uint64_t x) { return (x + 7u) & ~7ull; }
 
 // ---- mirsha_staging.hip
