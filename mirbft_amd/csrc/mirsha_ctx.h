@@ -162,6 +162,11 @@ struct mirsha_ctx {
     // stream, so chunk k's digests return while chunk k+1's bytes go in.
     hipStream_t xin = nullptr, xout = nullptr;
     std::vector<hipEvent_t> xev;  // per-call events (grow-only pool)
+    // Host scratch of the synchronous slice call (request lengths, packed
+    // offsets), kept across calls: fresh vectors cost ~1-2 ms of page faults
+    // and zeroing per 2^20 requests.
+    std::vector<uint32_t> sl_len;
+    std::vector<uint64_t> sl_poff;
     KernelTimer timers[6];         // msgs, lists, gen, chain, fused, overlap
     AsyncSlot slots[kAsyncSlots];
     uint64_t next_ticket = 1;  // ticket of the next submission

@@ -643,12 +643,16 @@ int run_arena_call(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, cons
 // Validates a slice-list request set and returns each request's total length.
 // The first request with a per-request slice error (err[i]: 0 ok, 1 not
 // monotone, 2 NULL slice, 3 too long), reported as the call's error.
+int slice_errors_at(mirsha_ctx* c, uint8_t code, uint32_t i) {
+    if (code == 1) return fail(c, MIRSHA_EINVAL, "slice_first not monotone at request %u", i);
+    if (code == 2) return fail(c, MIRSHA_EINVAL, "request %u has a NULL slice", i);
+    if (code == 3) return fail(c, MIRSHA_ERANGE, "request %u exceeds %u bytes", i, MIRSHA_MAX_MESSAGE_BYTES);
+    return MIRSHA_OK;
+}
+
 int slice_errors(mirsha_ctx* c, const uint8_t* err, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++) {
-        if (err[i] == 1) return fail(c, MIRSHA_EINVAL, "slice_first not monotone at request %u", i);
-        if (err[i] == 2) return fail(c, MIRSHA_EINVAL, "request %u has a NULL slice", i);
-        if (err[i] == 3) return fail(c, MIRSHA_ERANGE, "request %u exceeds %u bytes", i, MIRSHA_MAX_MESSAGE_BYTES);
-    }
+    for (uint32_t i = 0; i < n; i++)
+        if (err[i]) return slice_errors_at(c, err[i], i);
     return MIRSHA_OK;
 }
 
@@ -665,23 +669,45 @@ int slice_lengths(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t
                   const uint32_t* slice_first, uint32_t n, const uint8_t* out, std::vector<uint32_t>& len) {
     if (int rc = slice_args(c, slice_ptr, slice_len, slice_first, n, out)) return rc;
     const uint32_t ns = slice_first[n];
-    len.resize(n);
-    // err[i]: 0 ok, 1 not monotone, 2 NULL slice, 3 too long (first error reported)
-    std::vector<uint8_t> err(n, 0);
+    if (len.size() < n) len.resize(n);  // grow-only: a reused vector is not cleared
+    // The first bad request of each thread's range, and its code (1 not
+    // monotone, 2 NULL slice, 3 too long); the lowest index is reported.
     const uint64_t meta = 16ull * (ns > slice_first[0] ? ns : 0u);
-    mirsha::host::parallel_for(n, mirsha::host::threads_for(meta, n), [&](uint32_t lo, uint32_t hi) {
+    const int T = mirsha::host::threads_for(meta, n);
+    std::vector<uint32_t> bad(std::max(T, 1), UINT32_MAX);
+    std::vector<uint8_t> code(std::max(T, 1), 0);
+    const uint32_t step = (n + (uint32_t)std::max(T, 1) - 1) / (uint32_t)std::max(T, 1);
+    mirsha::host::parallel_for(n, T, [&](uint32_t lo, uint32_t hi) {
+        const uint32_t k = lo / std::max<uint32_t>(step, 1);
         for (uint32_t i = lo; i < hi; i++) {
-            if (slice_first[i + 1] < slice_first[i] || slice_first[i + 1] > ns) { err[i] = 1; continue; }
+            uint8_t e = 0;
             uint64_t L = 0;
-            for (uint32_t s = slice_first[i]; s < slice_first[i + 1]; s++) {
-                if (slice_len[s] && !slice_ptr[s]) { err[i] = 2; break; }
-                L += slice_len[s];
+            if (slice_first[i + 1] < slice_first[i] || slice_first[i + 1] > ns) {
+                e = 1;
+            } else {
+                for (uint32_t s = slice_first[i]; s < slice_first[i + 1]; s++) {
+                    if (slice_len[s] && !slice_ptr[s]) { e = 2; break; }
+                    L += slice_len[s];
+                }
+                if (!e && L > MIRSHA_MAX_MESSAGE_BYTES) e = 3;
             }
-            if (!err[i] && L > MIRSHA_MAX_MESSAGE_BYTES) err[i] = 3;
+            if (e) {
+                bad[k] = i;
+                code[k] = e;
+                return;
+            }
             len[i] = (uint32_t)L;
         }
     });
-    return slice_errors(c, err.data(), n);
+    uint32_t first_bad = UINT32_MAX;
+    uint8_t first_code = 0;
+    for (size_t k = 0; k < bad.size(); k++)
+        if (bad[k] < first_bad) {
+            first_bad = bad[k];
+            first_code = code[k];
+        }
+    if (first_bad == UINT32_MAX) return MIRSHA_OK;
+    return slice_errors_at(c, first_code, first_bad);
 }
 
 }  // namespace mirsha_api
@@ -704,13 +730,14 @@ int mirsha_hash_slices(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uin
     if (n == 0) return MIRSHA_OK;
     const auto t0 = Clock::now();
     for (double& x : c->prof) x = 0.0;
-    std::vector<uint32_t> len;
+    std::vector<uint32_t>& len = c->sl_len;
     if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     c->prof[MIRSHA_PROF_VALIDATE] = ms_since(t0);
     if (int rc = use_device(c)) return rc;
     // One packing pass, by threads, straight into pinned staging (the Go
     // side's single copy), chunk by chunk behind the DMA of the previous one.
-    std::vector<uint64_t> poff(n);
+    std::vector<uint64_t>& poff = c->sl_poff;
+    if (poff.size() < n) poff.resize(n);
     const uint64_t p = mirsha::host::exclusive_scan(len.data(), n, poff.data());
     ArenaSrc src;
     src.ptr = slice_ptr;
