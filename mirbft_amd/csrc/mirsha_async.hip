@@ -54,10 +54,10 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     // fingerprint collisions, rare) follow in one second launch.
     const bool dedup = (flags & MIRSHA_SUBMIT_DEDUP) && n > 1;
     double ph[MIRSHA_PROF_PHASES] = {};
-    std::vector<uint32_t> len;
+    std::vector<uint32_t>& len = c->sl_len;  // context scratch (single caller), grow-only
     if (dedup) {
         if (int rc = slice_args(c, slice_ptr, slice_len, slice_first, n, out)) return rc;
-        len.assign(n, 0u);
+        if (len.size() < n) len.resize(n);  // each segment's lengths are set before it is queued
     } else if (n) {
         if (int rc = slice_lengths(c, slice_ptr, slice_len, slice_first, n, out, len)) return rc;
     }
@@ -76,15 +76,8 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
     // digests into rows [row0, row0 + m) of sl.dig.
     auto queue = [&](const uint32_t* ids, uint32_t m, uint32_t row0, PinnedBuf& stage, DevBuf& dev) -> int {
         const auto tq = Clock::now();
-        std::vector<uint64_t> poff(m);
-        std::vector<uint32_t> plen(m);
         uint64_t bytes = 0;
-        for (uint32_t k = 0; k < m; k++) {
-            const uint32_t i = ids ? ids[k] : k;
-            poff[k] = bytes;
-            plen[k] = len[i];
-            bytes += len[i];
-        }
+        for (uint32_t k = 0; k < m; k++) bytes += len[ids ? ids[k] : k];
         if (bytes + kArenaSlack > MIRSHA_MAX_DEVICE_ARENA_BYTES)
             return fail(c, MIRSHA_ERANGE, "submission of %llu bytes exceeds one device arena (%u); split it",
                         (unsigned long long)bytes, MIRSHA_MAX_DEVICE_ARENA_BYTES);
@@ -94,11 +87,19 @@ int async_submit(mirsha_ctx* c, const uint8_t* const* slice_ptr, const uint64_t*
         HIP_TRY(c, stage.ensure(o_end));
         HIP_TRY(c, dev.ensure(o_dig + 32ull * std::max<uint32_t>(m, 1)));
         uint8_t* st = stage.as<uint8_t>();
-        mirsha::host::pack(slice_ptr, slice_len, slice_first, ids, m, poff.data(), st,
-                           mirsha::host::threads_for(bytes, m), true);
-        memcpy(st + o_off, poff.data(), 8ull * m);
-        memcpy(st + o_len, plen.data(), 4ull * m);
-        const bool identity = bucket_order(plen.data(), m, reinterpret_cast<uint32_t*>(st + o_ord));
+        // offsets and lengths straight into the staged metadata (no temporaries)
+        uint64_t* poff = reinterpret_cast<uint64_t*>(st + o_off);
+        uint32_t* plen = reinterpret_cast<uint32_t*>(st + o_len);
+        uint64_t p = 0;
+        for (uint32_t k = 0; k < m; k++) {
+            const uint32_t i = ids ? ids[k] : k;
+            poff[k] = p;
+            plen[k] = len[i];
+            p += len[i];
+        }
+        mirsha::host::pack(slice_ptr, slice_len, slice_first, ids, m, poff, st, mirsha::host::threads_for(bytes, m),
+                           true);
+        const bool identity = bucket_order(plen, m, reinterpret_cast<uint32_t*>(st + o_ord));
         uint8_t* dv = dev.as<uint8_t>();
         if (m) {
             HIP_TRY(c, hipMemcpyAsync(dv, st, o_end, hipMemcpyHostToDevice, c->stream));
