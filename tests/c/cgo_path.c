@@ -174,11 +174,17 @@ static void part_range(uint32_t lo, uint32_t hi, int part, int parts, uint32_t* 
 typedef struct {
     const Request* reqs;
     uint8_t* arena;
-    const uint64_t* off;
+    uint64_t* off;
     uint32_t lo, hi;
     const uint8_t* dsrc;
     uint8_t* ddst;
     uint32_t dlo, dhi;
+    /* chunked form: the chunk is blocks [blo, bhi) of br requests each; the
+     * workers write off[i] of their blocks from the blocks' byte prefix bpre
+     * (the offsets pass folded into the packing) */
+    const uint64_t* bpre;
+    const uint32_t* lens;
+    uint32_t n, br, blo, bhi;
 } ChunkJob;
 
 /* pack_stores "nt": each worker gathers its requests in a 16 KiB window and
@@ -232,7 +238,20 @@ static void chunk_part_nt(const ChunkJob* j, uint32_t a, uint32_t b) {
 static void chunk_part(void* arg, int part, int parts) {
     const ChunkJob* j = (const ChunkJob*)arg;
     uint32_t a, b;
-    part_range(j->lo, j->hi, part, parts, &a, &b);
+    if (j->bpre) {
+        uint32_t ba, bb;
+        part_range(j->blo, j->bhi, part, parts, &ba, &bb);
+        a = ba * j->br < j->n ? ba * j->br : j->n;
+        b = bb * j->br < j->n ? bb * j->br : j->n;
+        if (ba >= bb) a = b = 0;
+        uint64_t p = j->bpre[ba];
+        for (uint32_t i = a; i < b; i++) {
+            j->off[i] = p;
+            p += j->lens[i];
+        }
+    } else {
+        part_range(j->lo, j->hi, part, parts, &a, &b);
+    }
     if (g_nt) {
         chunk_part_nt(j, a, b);
         a = b;
@@ -260,51 +279,44 @@ static uint64_t offsets(const Request* reqs, uint32_t n, uint64_t* off, uint32_t
     return p;
 }
 
-/* offsets by the pool: a two-pass scan (lengths and per-part sums, then the
- * offsets of each part from the prefix of the sums) */
+/* The chunked form's one pass before packing: lens[i] and the byte sum of
+ * every block of br requests (at most MAX_BLOCKS blocks), by the pool; the
+ * caller turns the sums into each block's starting offset.  The offsets
+ * themselves are written by the packing workers (chunk_part). */
+#define MAX_BLOCKS 4096
 typedef struct {
     const Request* reqs;
-    uint32_t n;
-    uint64_t* off;
+    uint32_t n, br, nb;
     uint32_t* lens;
-    uint64_t part_sum[65];
-} OffJob;
+    uint64_t bpre[MAX_BLOCKS + 1];
+} LenJob;
 
-static void off_sum_part(void* arg, int part, int parts) {
-    OffJob* j = (OffJob*)arg;
-    uint32_t a, b;
-    part_range(0, j->n, part, parts, &a, &b);
-    uint64_t s = 0;
-    for (uint32_t i = a; i < b; i++) {
-        const uint64_t l = j->reqs[i].len[0] + j->reqs[i].len[1] + j->reqs[i].len[2];
-        j->lens[i] = (uint32_t)l;
-        s += l;
-    }
-    j->part_sum[part + 1] = s;
-}
-
-static void off_write_part(void* arg, int part, int parts) {
-    OffJob* j = (OffJob*)arg;
-    uint32_t a, b;
-    part_range(0, j->n, part, parts, &a, &b);
-    uint64_t p = j->part_sum[part];
-    for (uint32_t i = a; i < b; i++) {
-        j->off[i] = p;
-        p += j->lens[i];
+static void len_part(void* arg, int part, int parts) {
+    LenJob* j = (LenJob*)arg;
+    uint32_t ba, bb;
+    part_range(0, j->nb, part, parts, &ba, &bb);
+    for (uint32_t blk = ba; blk < bb; blk++) {
+        const uint32_t a = blk * j->br, b = a + j->br < j->n ? a + j->br : j->n;
+        uint64_t s = 0;
+        for (uint32_t i = a; i < b; i++) {
+            const uint64_t l = j->reqs[i].len[0] + j->reqs[i].len[1] + j->reqs[i].len[2];
+            j->lens[i] = (uint32_t)l;
+            s += l;
+        }
+        j->bpre[blk + 1] = s;
     }
 }
 
-static uint64_t offsets_parallel(const Request* reqs, uint32_t n, uint64_t* off, uint32_t* lens, Pool* pool) {
-    static OffJob j;
-    j.reqs = reqs;
-    j.n = n;
-    j.off = off;
-    j.lens = lens;
-    j.part_sum[0] = 0;
-    pool_run(pool, off_sum_part, &j);
-    for (int k = 0; k < pool->n; k++) j.part_sum[k + 1] += j.part_sum[k];
-    pool_run(pool, off_write_part, &j);
-    return j.part_sum[pool->n];
+static uint64_t lengths_parallel(const Request* reqs, uint32_t n, uint32_t* lens, Pool* pool, LenJob* j) {
+    j->reqs = reqs;
+    j->n = n;
+    j->br = (n + MAX_BLOCKS - 1) / MAX_BLOCKS;
+    j->nb = (n + j->br - 1) / j->br;
+    j->lens = lens;
+    j->bpre[0] = 0;
+    pool_run(pool, len_part, j);
+    for (uint32_t k = 0; k < j->nb; k++) j->bpre[k + 1] += j->bpre[k];
+    return j->bpre[j->nb];
 }
 
 /* Round 2 / round 4 HashBatch: pack everything (1 or `pool` workers), one
@@ -313,7 +325,7 @@ static void hash_batch_onecall(const Request* reqs, uint32_t n, uint8_t* arena, 
                                uint8_t* dig, Pool* pool, double* pack_ms, double* call_ms) {
     const double t0 = now_ms();
     const uint64_t total = offsets(reqs, n, off, lens);
-    ChunkJob j = {reqs, arena, off, 0, n, NULL, NULL, 0, 0};
+    ChunkJob j = {reqs, arena, off, 0, n, NULL, NULL, 0, 0, NULL, NULL, 0, 0, 0, 0};
     if (pool)
         pool_run(pool, chunk_part, &j);
     else
@@ -352,39 +364,35 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
                                uint8_t* dig_pinned, uint8_t* dig, Pool* pool, uint64_t chunk_bytes, mirsha_multi* m,
                                double* pack_ms, double* call_ms, int* chunks_out) {
     static uint64_t ticket[MAX_CHUNKS];
-    static uint32_t cfirst[MAX_CHUNKS + 1];
+    static uint32_t cfirst[MAX_CHUNKS + 1], cblk[MAX_CHUNKS + 1];
+    static LenJob lj;
     const double t0 = now_ms();
-    const uint64_t total = offsets_parallel(reqs, n, off, lens, pool);
+    const uint64_t total = lengths_parallel(reqs, n, lens, pool, &lj);
     ph_off = now_ms() - t0;
     ph_pack = ph_submit = ph_max_submit = ph_max_pool = 0.0;
-    /* chunk boundaries: requests [lo, hi) until the chunk's bytes reach the
-     * budget */
+    /* chunk boundaries at block granularity: blocks [b0, b1) until the
+     * chunk's bytes reach the budget -- a quarter, a half, then whole budgets:
+     * the link starts early and stays busy while the workers pack the next,
+     * larger chunk */
     int nk = 0;
-    for (uint32_t lo = 0; lo < n;) {
-        /* a quarter, a half, then whole budgets: the link starts early and
-         * stays busy while the workers pack the next, larger chunk */
+    for (uint32_t b0 = 0; b0 < lj.nb;) {
         const uint64_t budget = nk == 0 ? chunk_bytes / 4 : nk == 1 ? chunk_bytes / 2 : chunk_bytes;
-        /* hi = the first index past lo with off[hi] - off[lo] >= budget, else n
-         * (binary search: off is nondecreasing) */
-        uint32_t hi = lo + 1, top = n;
-        while (hi < top) {
-            const uint32_t mid = hi + (top - hi) / 2;
-            if (off[mid] - off[lo] < budget)
-                hi = mid + 1;
-            else
-                top = mid;
-        }
+        uint32_t b1 = b0 + 1;
+        while (b1 < lj.nb && lj.bpre[b1] - lj.bpre[b0] < budget) b1++;
         if (nk == MAX_CHUNKS) exit(6);
-        cfirst[nk++] = lo;
-        lo = hi;
+        cblk[nk] = b0;
+        cfirst[nk++] = b0 * lj.br;
+        b0 = b1;
     }
+    cblk[nk] = lj.nb;
     cfirst[nk] = n;
     int copied = 0; /* chunks whose digests are in dig */
     ChunkJob job;
     for (int k = 0; k <= nk; k++) {
         /* workers: pack chunk k (if any) + the digests of chunks already back */
         const double tp = now_ms();
-        job = (ChunkJob){reqs, arena, off, k < nk ? cfirst[k] : 0, k < nk ? cfirst[k + 1] : 0, dig_pinned, dig, 0, 0};
+        job = (ChunkJob){reqs, arena, off, k < nk ? cfirst[k] : 0, k < nk ? cfirst[k + 1] : 0, dig_pinned, dig, 0, 0,
+                         lj.bpre, lens, n, lj.br, k < nk ? cblk[k] : 0, k < nk ? cblk[k + 1] : 0};
         int upto = copied;
         while (upto < k - 1) {
             int done = 0;
@@ -424,7 +432,7 @@ static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, 
             CHECK(mirsha_wait(ctx, ticket[nk - 1]));
         const double tw = now_ms();
         ph_wait = tw - t1;
-        job = (ChunkJob){reqs, arena, off, 0, 0, dig_pinned, dig, cfirst[copied], n};
+        job = (ChunkJob){reqs, arena, off, 0, 0, dig_pinned, dig, cfirst[copied], n, NULL, NULL, 0, 0, 0, 0};
         pool_run(pool, chunk_part, &job);
         ph_copy = now_ms() - tw;
     }

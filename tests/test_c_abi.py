@@ -72,10 +72,20 @@ def test_cgo_path_on_gpu(tmp_path, stores):
     assert r.returncode == 0, r.stderr
     line = json.loads(r.stdout.splitlines()[-1])
     assert line["requests"] == n and line["parallel"]["ms"] > 0 and line["pack_stores"] == stores
-    # requests per chunk (a chunk ends at a request boundary; the first two
-    # have a quarter and a half of the budget)
-    per, first, second = (-(-(1 << b) // (16 + data_len)) for b in (20, 18, 19))
-    assert line["parallel"]["chunks"] == 2 + -(-(n - first - second) // per) == line["multi"]["chunks"] == 28
+    # chunks end at block boundaries (blocks of ceil(n / 4096) requests); the
+    # first two have a quarter and a half of the budget
+    br = -(-n // 4096)
+    nb = -(-n // br)
+    bsum = [min(br, n - b * br) * (16 + data_len) for b in range(nb)]
+    want_chunks, b0 = 0, 0
+    while b0 < nb:
+        budget = (1 << 20) >> (2 - want_chunks) if want_chunks < 2 else 1 << 20
+        acc, b1 = bsum[b0], b0 + 1
+        while b1 < nb and acc < budget:
+            acc += bsum[b1]
+            b1 += 1
+        want_chunks, b0 = want_chunks + 1, b1
+    assert line["parallel"]["chunks"] == want_chunks == line["multi"]["chunks"] > 20
     arena = oracle_py.gen_requests(0x6D69726266740002, 0, 4, data_len)
     stride = 16 + data_len
     want = oracle_py.hash_requests(arena, np.arange(4, dtype=np.uint64) * stride, np.full(4, stride))
