@@ -330,7 +330,7 @@ int async_submit_arena(mirsha_ctx* c, const uint8_t* arena, uint64_t arena_len, 
     // 8-15 ms (profiles/r05w: 13-22 ms calls of the chunked HashBatch); with
     // one copy stream no call stalled, at the same steady-state speed.
     uint8_t* kout = nullptr;
-    if (sl.direct && n && kernel_writable_host(out, c->device)) {
+    if (sl.direct && n && (reinterpret_cast<uintptr_t>(out) & 15u) == 0 && kernel_writable_host(out, c->device)) {
         void* dp = nullptr;
         if (hipHostGetDevicePointer(&dp, out, 0) == hipSuccess)
             kout = static_cast<uint8_t*>(dp);

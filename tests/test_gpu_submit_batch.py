@@ -146,3 +146,22 @@ def test_size_limits_rejected_before_any_read(engine):
     src, off, lens = _cycle(32, 50)
     t = engine.submit_batch(src, off, lens)
     assert np.array_equal(engine.wait(t), oracle_py.hash_requests(src, off, lens))
+
+
+def test_pinned_outputs_at_any_alignment(engine):
+    """A page-locked digests_out is written by the kernel when 16-byte
+    aligned, else by a D2H copy: both bit-exact, at offsets 0, 16 and 1 of a
+    mirsha_host_alloc buffer, with a pinned and a pageable arena."""
+    src, off, lens = _cycle(41, 3000, big_every=700, big_len=70_000)
+    n = off.size
+    want = oracle_py.hash_requests(src, off, lens, threads=8)
+    pinned = engine.host_empty(src.size)
+    pinned[:] = src
+    for arena in (src, pinned):
+        for shift in (0, 16, 1):
+            buf = engine.host_empty(32 * n + 32)
+            out = buf[shift:shift + 32 * n].reshape(n, 32)
+            t = engine.submit_batch(arena, off, lens, out=out)
+            got = engine.wait(t)
+            assert np.array_equal(got, want), f"shift {shift}"
+            assert np.array_equal(out, want)
