@@ -219,6 +219,37 @@ def _time_cpu(fn, seconds, threads_list):
     return res
 
 
+def check_windows(n_batches, batch_size, seed, per_window=256):
+    """Batch ranges [b0, b1) the self-check samples: the first window, the
+    last (it ends with the final batch, which is short when BatchSize does not
+    divide the request count) and 4 random ones, each ~per_window requests."""
+    k = max(1, per_window // max(batch_size, 1))
+    if n_batches <= 0:
+        return []
+    rng = np.random.default_rng(seed)
+    hi = max(n_batches - k, 0)
+    starts = {0, hi} | {int(x) for x in rng.integers(0, hi + 1, size=4)}
+    return [(b0, min(b0 + k, n_batches)) for b0 in sorted(starts)]
+
+
+def check_batch_windows(seed, first_req, data_len, idx, first, req_digests, bat_digests):
+    """Compare request digests [first[b0], first[b1]) and batch digests
+    [b0, b1) of every check_windows window with the oracle (generator ->
+    oracle_hash_requests -> oracle_batch_digests).  req_digests / bat_digests:
+    (n, 32) / (n_batches, 32) host arrays of the rank's own range."""
+    o = _oracle()
+    stride = 16 + data_len
+    ok = True
+    for b0, b1 in check_windows(first.size - 1, int(first[1] - first[0]) if first.size > 1 else 1, first_req + 17):
+        i0, i1 = int(first[b0]), int(first[b1])
+        arena = o.gen_requests(seed, first_req + i0, i1 - i0, data_len)
+        want = o.hash_requests(arena, np.arange(i1 - i0, dtype=np.uint64) * stride, np.full(i1 - i0, stride))
+        ok = ok and bool(np.array_equal(req_digests[i0:i1], want))
+        wb = o.batch_digests(want, idx[i0:i1].astype(np.int64) - i0, first[b0:b1 + 1].astype(np.int64) - i0)
+        ok = ok and bool(np.array_equal(bat_digests[b0:b1], wb))
+    return ok
+
+
 class BatchWorkload:
     """Configs 2 and 3: a dense stream of equal-size requests + batch lists."""
 
@@ -298,18 +329,12 @@ class BatchWorkload:
         return self.eng.kernel_time(KERNEL_LISTS)[1] + self.eng.kernel_time(KERNEL_CHAIN)[1]
 
     def self_check(self):
-        o = _oracle()
-        k = 256
-        arena = o.gen_requests(self.seed, self.first_req, k, self.data_len)
-        want = o.hash_requests(arena, np.arange(k, dtype=np.uint64) * self.stride, np.full(k, self.stride))
-        ok = bool(np.array_equal(self.d_req[:k].cpu().numpy(), want))
-        # and the first batch digests over those requests
-        nb = int(np.searchsorted(self.first, k, side="right")) - 1
-        if nb > 0:
-            torch.cuda.synchronize(self.d_req.device)
-            wb = o.batch_digests(want, self.idx[: self.first[nb]], self.first[: nb + 1])
-            ok = ok and bool(np.array_equal(self.d_bat[:nb].cpu().numpy(), wb))
-        return ok
+        """This rank's last step against the oracle: request and batch digests
+        of batch-aligned windows (check_windows: the first, the last -- which
+        holds the final, possibly partial batch -- and 4 random ones)."""
+        torch.cuda.synchronize(self.d_req.device)
+        return check_batch_windows(self.seed, self.first_req, self.data_len, self.idx, self.first,
+                                   self.d_req.cpu().numpy(), self.d_bat.cpu().numpy())
 
     def pcie(self):
         n, stride = self.n, self.stride
@@ -480,6 +505,23 @@ class BatchWorkload:
                          "the reference's Go 1.13/1.14 crypto/sha256 on amd64 (.travis.yml:5-6, go.mod:3), whose "
                          "AVX2/BMI2 block function vectorises the message schedule and has no SHA-NI path "
                          "(Go added SHA-NI in 1.21)"}
+        # BASELINE.md's labelled stand-in: the same loop through OpenSSL EVP
+        # (oracle/evp_loop.c: three Writes per request, one per RequestAck
+        # digest), on the same sample, 1 core; then the pool legs below.
+        def evp(threads, arena=arena, off=off, ln=ln, idx=idx, first=first):
+            d = o.evp_hash_requests(arena, off, ln, threads=threads)
+            o.evp_batch_digests(d, idx, first)
+
+        evp_ok = bool(np.array_equal(o.evp_hash_requests(arena[: 64 * stride], off[:64], ln[:64]),
+                                     o.hash_requests(arena[: 64 * stride], off[:64], ln[:64])))
+        de, dte = _time_cpu(evp, seconds / 4, (1,))[1]
+        openssl = {"value": de * per / dte, "unit": "digests/s", "cores": 1,
+                   "label": "OpenSSL stand-in for Go crypto/sha256",
+                   "openssl": o.evp_version(), "matches_oracle": evp_ok,
+                   "sample": f"{de} passes of the headline sample, {dte:.1f} s",
+                   "note": "BASELINE.md CPU-baseline plan: processor.go:133-143 with EVP_DigestInit_ex2 / "
+                           "EVP_DigestUpdate per HashRequest.Data slice (3 per request, state_machine.go:313-317) / "
+                           "EVP_DigestFinal_ex; batch digests one Update per RequestAck digest (oracle/evp_loop.c)"}
         # Pool legs on a larger sample (whole config up to 2^20 requests), so
         # per-pass thread start-up is noise; batch digests single-threaded, as
         # the state machine consumes them (processResults, state_machine.go:377-433).
@@ -503,6 +545,9 @@ class BatchWorkload:
             r = _time_cpu(pool, seconds / 3, (t,))[t]
             legs[name] = {"value": r[0] * pper / r[1], "threads": t,
                           "sample": f"{r[0]} passes x {npool} requests + {pfirst.size - 1} batch digests, {r[1]:.1f} s"}
+            re = _time_cpu(lambda th: evp(th, parena, poff, pln, pidx, pfirst), seconds / 6, (t,))[t]
+            openssl.setdefault("pool", {})[name] = {"value": re[0] * pper / re[1], "threads": t,
+                                                    "sample": f"{re[0]} passes of the pool sample, {re[1]:.1f} s"}
         return {
             "value": done1 * per / dt1, "unit": "digests/s", "cores": 1, "kind": "port",
             "sample": f"{done1} passes x ({n} requests x {stride} B + {first.size - 1} BatchSize-{bs} batch "
@@ -510,6 +555,7 @@ class BatchWorkload:
                       f"SHA-NI compression (faster than the reference's Go 1.14 crypto/sha256, which has no "
                       f"SHA-NI path: a conservative baseline; the Go 1.14-class figure is go114_class)",
             "go114_class": go114,
+            "openssl_evp": openssl,
             "pool": {**legs,
                      "note": "order-preserving ProcessorWorkPool analogue (processor.go:312-361): workers pull "
                              "requests from a shared counter; numcpu = HashWorkers = runtime.NumCPU() = the affinity "
@@ -530,8 +576,9 @@ class BatchWorkload:
         ONE launch per cycle hashes the cycle's requests and the previous
         cycle's batches, as a stream of Ready() cycles pipelines (the state
         machine batches digests of earlier cycles).  Measured after the
-        headline steps on rank 0: wall time of --steps launches (no events),
-        then the kernel's event time in a second pass."""
+        headline steps on rank 0: --steps launches with the kernel's HIP
+        events on, wall time and kernel time from that ONE pass (kernel <=
+        wall holds by construction)."""
         if self.plan is None or self.overlap:
             return None
         timer = KERNEL_FUSED if self.plan.mode_name == "fused" else KERNEL_OVERLAP
@@ -550,28 +597,28 @@ class BatchWorkload:
         for _ in range(max(self.a.warmup, 2)):
             launch()
         torch.cuda.synchronize(dev)
+        e.set_timing_mask([timer])
+        e.set_timing(True)
+        e.reset_timing()
         t0 = time.perf_counter()
         for _ in range(steps):
             launch()
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
-        e.set_timing_mask([timer])
-        e.set_timing(True)
-        e.reset_timing()
-        for _ in range(steps):
-            launch()
-        torch.cuda.synchronize(dev)
         e.set_timing(False)
         n_o, ms_o = e.kernel_time(timer)
         e.set_timing_mask(range(32))
         kms = ms_o / max(n_o, 1)
-        tops = (self.req_blocks + self.bat_blocks) * OPS_PER_COMPRESSION / (kms * 1e-3) / 1e12
+        work = (self.req_blocks + self.bat_blocks) * OPS_PER_COMPRESSION
+        tops = work / (kms * 1e-3) / 1e12
+        step_tops = work / (dt / steps) / 1e12
         return {"digests_per_s": self.digests * steps / dt, "ms_per_step": dt / steps * 1e3,
                 "kernel": {KERNEL_FUSED: "sha256_fused_paced_kernel"}.get(timer, "sha256_msgs_overlap_kernel"),
-                "avg_launch_ms": kms, "frac": tops / VALU_PEAK_TOPS,
+                "avg_launch_ms": kms, "frac": tops / VALU_PEAK_TOPS, "step_frac": step_tops / VALU_PEAK_TOPS,
                 "note": "one launch per cycle: this cycle's requests + the previous cycle's batch chains "
                         "(mirsha_pipeline_overlap_device, on this plan), steady state of a cycle stream; "
-                        "frac over both"}
+                        "frac = both over the kernel's event time, step_frac = both over ms_per_step; "
+                        "one pass, events on"}
 
     def extra(self):
         mode = self.plan.mode_name if self.plan is not None else "none"
@@ -652,8 +699,9 @@ class MixedWorkload:
 
     def self_check(self):
         o = _oracle()
-        rng = np.random.default_rng(5)
-        ids = np.sort(rng.choice(self.n, size=min(256, self.n), replace=False))
+        rng = np.random.default_rng(5 + self.first_req)
+        ends = np.r_[np.arange(min(8, self.n)), np.arange(max(self.n - 8, 0), self.n)]  # the range's first / last
+        ids = np.unique(np.r_[ends, rng.choice(self.n, size=min(256, self.n), replace=False)])
         arena, off, ln = o.gen_mixed(self.seed, ids + self.first_req)
         if not np.array_equal(ln, self.ln[ids]):
             return False
@@ -900,18 +948,22 @@ def config3_leg(a, eng, dev):
         tops = work_blocks * OPS_PER_COMPRESSION / (ms_k / steps * 1e-3) / 1e12
         tkey = kernel_source_key(a.variant)
         traffic, _ = lookup_traffic(a.traffic_file, tkey, 3, kname)
+        step_tops = (wl.req_blocks + wl.bat_blocks) * OPS_PER_COMPRESSION / (dt / steps * 1e-3) / 1e12
         leg = {"plan": wl.plan.mode_name, "ms_per_step": dt / steps * 1e3,
                "digests_per_s": wl.digests * steps / dt, "kernel": kname, "avg_launch_ms": kms,
-               "frac": tops / VALU_PEAK_TOPS, "compressions": work_blocks, "traffic": traffic,
-               "traffic_key": tkey}
+               "frac": tops / VALU_PEAK_TOPS, "step_frac": step_tops / VALU_PEAK_TOPS,
+               "compressions": work_blocks, "step_compressions": wl.req_blocks + wl.bat_blocks,
+               "traffic": traffic, "traffic_key": tkey}
         if wl.plan.mode_name == "fused":
             # right behind the timed steps, the chip still at this load's clock
             # (a self-check first left it idle and cooling: profiles/r04g)
             a3.warmup = 30
             leg["overlap_cycles"] = wl.overlap_cycles()
-            leg["frac_note"] = "request + VerifyBatch compressions over the fused launch's time"
+            leg["frac_note"] = ("frac: request + VerifyBatch compressions over the fused launch's time; step_frac: "
+                                "the same over ms_per_step")
         else:
-            leg["frac_note"] = "request compressions over the request kernel's time (the batch chains follow)"
+            leg["frac_note"] = ("frac: request compressions over the request kernel's time (the batch chains "
+                                "follow); step_frac: request + VerifyBatch compressions over ms_per_step")
             leg["batch_kernel_ms"] = wl.batch_ms() / steps
         eng.set_timing_mask(range(32))
         leg["self_check"] = wl.self_check()
@@ -932,19 +984,32 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def count_devices():
+    """Visible GPUs, counted in a throwaway child process: this launching
+    parent never imports torch and never initialises the HIP runtime (on ROCm
+    torch.cuda.device_count() falls back to hipGetDeviceCount when amdsmi is
+    absent, which would start the runtime in the process that forks the
+    ranks).  0 when the child fails (no GPU, no torch)."""
+    if os.environ.get("MIRSHA_BENCH_COUNT_STUB"):  # CPU tests: the count the child would print
+        return int(os.environ["MIRSHA_BENCH_COUNT_STUB"])
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.split()[-1]) if r.returncode == 0 else 0
+    except (IndexError, ValueError):
+        return 0
+
+
 def launch_ranks(a):
     """`--gpus N` without a launcher: start N rank processes of this script
     (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rendezvous on 127.0.0.1),
     forward rank 0's stdout, and return non-zero if any rank fails (the others
-    are then stopped by PID).  The parent only counts devices
-    (torch.cuda.device_count(), which does not initialise the GPU) and never
-    execs: the ranks are children."""
+    are then stopped by PID).  The parent only counts devices, in a child
+    process (count_devices), and never execs: the ranks are children."""
     n = a.gpus
     rehearsal = bool(os.environ.get("MIRSHA_BENCH_DEVICE"))
     if not rehearsal and not a.launch_check:
-        import torch as _torch
-
-        vis = _torch.cuda.device_count()
+        vis = count_devices()
         if vis < n:
             print(f"bench.py: --gpus {n} but {vis} device(s) visible (set MIRSHA_BENCH_DEVICE=<d> to rehearse "
                   f"{n} ranks on one device)", file=sys.stderr, flush=True)
@@ -999,6 +1064,25 @@ def launch_ranks(a):
     return rc
 
 
+def device_identity_check(per_rank, rehearsal):
+    """Whether the ranks ran on distinct GPUs, from the device UUIDs (else the
+    PCI bus ids) they report.  distinct: True / False, or None when the
+    identities are missing, or when MIRSHA_BENCH_DEVICE deliberately puts
+    every rank on one device (a rehearsal: not checked)."""
+    ids = []
+    for p in per_rank:
+        u = p.get("device_uuid") or ""
+        ids.append(u if u.strip("0-") else (str(p.get("pci_bus_id")) if p.get("pci_bus_id") is not None else None))
+    if len(per_rank) < 2:
+        return {"distinct": True, "note": "one rank"}
+    if rehearsal:
+        return {"distinct": None, "note": "rehearsal: every rank on device MIRSHA_BENCH_DEVICE, not checked"}
+    if any(i is None for i in ids):
+        return {"distinct": None, "note": "device identities unavailable"}
+    d = len(set(ids)) == len(ids)
+    return {"distinct": d, "note": f"{len(set(ids))} distinct device identities over {len(ids)} ranks"}
+
+
 def launch_check(a, world, rank):
     """--launch-check: the N>1 plumbing without a device (CPU tests): gloo
     rendezvous, barrier, each rank's request range (BatchWorkload's weak
@@ -1011,8 +1095,25 @@ def launch_check(a, world, rank):
     if os.environ.get("MIRSHA_BENCH_CHECK_SLEEP"):  # test hook: ranks that outlive a launcher's signal
         time.sleep(float(os.environ["MIRSHA_BENCH_CHECK_SLEEP"]))
     n = a.requests or CONFIGS[a.config if a.config in CONFIGS else 2][1]
+    # The per-rank self-check path on the CPU: this rank's range (at most 4,096
+    # requests of config 2's shape) hashed by the oracle stands in for the
+    # device digests; a test hook corrupts the final (partial) batch digest of
+    # one rank, which the AND over ranks must report.
+    from mirbft_amd import sharding as _sh
+
+    m = min(n, 4096)
+    data_len, bs = CONFIGS[2][0], CONFIGS[2][2]
+    seed, first_req = SEED_BASE + 2, rank * n
+    o = _oracle()
+    idx, first = _sh.batch_lists(m, bs)
+    req = o.hash_requests(o.gen_requests(seed, first_req, m, data_len), np.arange(m, dtype=np.uint64) * (16 + data_len),
+                          np.full(m, 16 + data_len))
+    bat = o.batch_digests(req, idx, first)
+    if os.environ.get("MIRSHA_BENCH_CHECK_CORRUPT_RANK") == str(rank):
+        bat[-1, 0] ^= 1
+    ok = check_batch_windows(seed, first_req, data_len, idx, first, req, bat)
     info = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
-            "first_request": rank * n, "requests": n}
+            "first_request": rank * n, "requests": n, "self_check": ok, "device_uuid": f"launch-check-{rank}"}
     per_rank = [info]
     if world > 1:
         per_rank = [None] * world
@@ -1021,7 +1122,11 @@ def launch_check(a, world, rank):
         print(json.dumps({"metric": "SHA-256 digests/s (request + batch digests), Actions.Hash stream",
                           "value": None, "unit": "digests/s", "n_gpus": world, "steps": a.steps,
                           "warmup": a.warmup, "launch_check": True, "per_rank": per_rank,
-                          "note": "launcher plumbing only: no device, no hashing"}), flush=True)
+                          "self_check": all(p["self_check"] for p in per_rank),
+                          "distributed": {"backend": "gloo" if world > 1 else None,
+                                          "device_identity": device_identity_check(per_rank, False)},
+                          "note": "launcher plumbing only: no device; self_check = the oracle's own digests of "
+                                  "each rank's range through the per-rank window check"}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -1042,13 +1147,16 @@ def main():
         launch_check(a, world, rank)
         return
     _import_product()
-    # Rehearsal knobs for the N>1 path on a one-GPU box (never set by the
-    # driver): every rank on device MIRSHA_BENCH_DEVICE, barriers and
-    # reductions over gloo instead of RCCL.
-    if os.environ.get("MIRSHA_BENCH_DEVICE"):
+    # Rehearsal knob for the N>1 path on a one-GPU box (never set by the
+    # driver): every rank on device MIRSHA_BENCH_DEVICE.  The control plane
+    # (barriers, max / sum of timings, the per-rank gather) is gloo at any N:
+    # the data path has no collective (north_star), so RCCL would carry only
+    # these few host scalars, and gloo is the branch every rehearsal ran.
+    # MIRSHA_BENCH_DIST_BACKEND=nccl is an A/B knob.
+    rehearsal = bool(os.environ.get("MIRSHA_BENCH_DEVICE"))
+    if rehearsal:
         local = int(os.environ["MIRSHA_BENCH_DEVICE"])
-    backend = os.environ.get("MIRSHA_BENCH_DIST_BACKEND",
-                             "gloo" if os.environ.get("MIRSHA_BENCH_DEVICE") else "nccl")
+    backend = os.environ.get("MIRSHA_BENCH_DIST_BACKEND", "gloo")
     dist = None
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -1155,12 +1263,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    # quick self-check of the last step against the CPU oracle on a sample
-    check_ok = wl.self_check() if rank == 0 else None
+    # Every rank checks the last step of its OWN request range against the CPU
+    # oracle on samples (first / last / random requests and the batches over
+    # them, the final partial batch included); the line's self_check is the
+    # AND over ranks, each rank's own is in per_rank.
+    check_ok = bool(wl.self_check())
 
     # Whole-job totals: the sum over ranks (config 5's block-balanced shards
-    # differ in request count per rank).
-    tot = torch.tensor([float(wl.digests), float(wl.bytes_hashed)], dtype=torch.float64, device=red_dev)
+    # differ in request count per rank).  step_compressions = every
+    # compression of a step (request + batch digests), BASELINE.md's per-config
+    # accounting, for roofline.step_frac.
+    step_comp = int(wl.req_blocks) + int(getattr(wl, "bat_blocks", 0))
+    tot = torch.tensor([float(wl.digests), float(wl.bytes_hashed), float(step_comp)], dtype=torch.float64,
+                       device=red_dev)
     if dist:
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     value = float(tot[0].item()) * a.steps / dt
@@ -1168,6 +1283,8 @@ def main():
     ms_per_step_k = ms_k / a.steps  # all launches of the dominant kernel in one step
     achieved_tops = work_blocks * OPS_PER_COMPRESSION / (ms_per_step_k * 1e-3) / 1e12
     hbm_gbs = hbm_bytes / (ms_per_step_k * 1e-3) / 1e9
+    # per-GPU average over the whole step's wall time (max over ranks)
+    step_tops = float(tot[2].item()) / world * OPS_PER_COMPRESSION / (dt / a.steps) / 1e12
 
     tkey = kernel_source_key(a.variant)
     traffic, tentry = lookup_traffic(a.traffic_file, tkey, a.config, kname)
@@ -1200,11 +1317,16 @@ def main():
                  "digests": int(wl.digests), "compressions": int(work_blocks),
                  "first_request": int(getattr(wl, "first_req", 0)), "wall_ms_per_step": dt_rank / a.steps * 1e3,
                  "kernel": kname, "kernel_avg_launch_ms": ms_k / max(n_k, 1),
-                 "frac": achieved_tops / VALU_PEAK_TOPS}
+                 "frac": achieved_tops / VALU_PEAK_TOPS, "self_check": check_ok}
     per_rank = [rank_info]
     if dist:
         per_rank = [None] * world
         dist.all_gather_object(per_rank, rank_info)
+    check_all = all(p["self_check"] for p in per_rank)
+    ident = device_identity_check(per_rank, rehearsal)
+    if ident["distinct"] is False:
+        raise SystemExit(f"bench.py: rank {rank}: ranks share a device ({ident['note']}); a multi-GPU line "
+                         f"needs one GPU per rank (MIRSHA_BENCH_DEVICE rehearses on one device)")
 
     if rank == 0:
         line = {
@@ -1233,6 +1355,12 @@ def main():
                 "peak": VALU_PEAK_TOPS,
                 "unit": "TOP/s",
                 "frac": achieved_tops / VALU_PEAK_TOPS,
+                "step_frac": step_tops / VALU_PEAK_TOPS,
+                "step_achieved": step_tops,
+                "step_compressions_per_gpu": float(tot[2].item()) / world,
+                "frac_note": "frac = the dominant kernel's compressions over its own HIP-event time; step_frac = "
+                             "every compression of a step (request + batch digests, BASELINE.md's accounting) "
+                             "over ms_per_step, per GPU",
                 "traffic": traffic,
                 "kernel": kname,
                 "avg_launch_ms": ms_k / max(n_k, 1),
@@ -1255,9 +1383,12 @@ def main():
             **wl.extra(),
             "events_in_timed_loop": bool(a.events_in_timed_loop),
             "timed_kernels": a.timed_kernels,
-            "self_check": check_ok,
+            "self_check": check_all,
+            "self_check_scope": "every rank: its own range's first and last batch-aligned windows (the final "
+                                "partial batch included) and 4 random ones, request + batch digests vs the oracle",
             "per_rank": per_rank,
             "distributed": {"world_size": world, "backend": backend if dist else None,
+                            "device_identity": ident,
                             "data_path_collectives": "none: each rank hashes its own request range; "
                                                      "barriers and max / sum reductions of timings only"},
             "pcie_inclusive": pcie,

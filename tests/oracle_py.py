@@ -130,6 +130,56 @@ def gen_mixed(seed: int, ids) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
     return arena[:total], off, ln
 
 
+EVP_SO = os.path.join(ORACLE_DIR, "libevp_loop.so")
+_evp = None
+
+
+def load_evp() -> ctypes.CDLL:
+    """oracle/libevp_loop.so: the reference loop through OpenSSL's EVP SHA-256
+    (BASELINE.md's "OpenSSL stand-in for Go crypto/sha256")."""
+    global _evp
+    if _evp is not None:
+        return _evp
+    src = os.path.join(ORACLE_DIR, "evp_loop.c")
+    if not os.path.exists(EVP_SO) or os.path.getmtime(EVP_SO) < os.path.getmtime(src):
+        build()
+    lib = ctypes.CDLL(EVP_SO)
+    vp = ctypes.c_void_p
+    lib.evp_hash_requests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int]
+    lib.evp_batch_digests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
+    lib.evp_version.restype = ctypes.c_char_p
+    _evp = lib
+    return lib
+
+
+def evp_hash_requests(arena, off, length, threads: int = 1, split: bool = True) -> np.ndarray:
+    """processor.go:133-143 through EVP (three Writes per request when split)."""
+    lib = load_evp()
+    a = np.ascontiguousarray(np.asarray(arena).reshape(-1).view(np.uint8))
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(length, dtype=np.uint32)
+    out = np.empty((o.size, 32), dtype=np.uint8)
+    if o.size and lib.evp_hash_requests(_p(a), _p(o), _p(ln), o.size, _p(out), int(threads), int(split)):
+        raise RuntimeError("evp_hash_requests failed")
+    return out
+
+
+def evp_batch_digests(req_digests: np.ndarray, idx, first) -> np.ndarray:
+    lib = load_evp()
+    d = np.ascontiguousarray(req_digests, dtype=np.uint8).reshape(-1, 32)
+    ix = np.ascontiguousarray(idx, dtype=np.uint32)
+    fs = np.ascontiguousarray(first, dtype=np.uint32)
+    nb = fs.size - 1
+    out = np.empty((nb, 32), dtype=np.uint8)
+    if nb and lib.evp_batch_digests(_p(d), _p(ix), _p(fs), nb, _p(out)):
+        raise RuntimeError("evp_batch_digests failed")
+    return out
+
+
+def evp_version() -> str:
+    return load_evp().evp_version().decode()
+
+
 def force_impl(impl: int) -> None:
     load().oracle_sha256_force_impl(impl)
 

@@ -36,6 +36,18 @@ def test_gpus_2_self_launches_two_ranks():
     assert len({p["pid"] for p in pr}) == 2 and os.getpid() not in {p["pid"] for p in pr}
     # weak scaling: rank r hashes its own request range
     assert [(p["first_request"], p["requests"]) for p in pr] == [(0, 1000), (1000, 1000)]
+    # every rank self-checks its own range; the line ANDs them (verdict r5 item 3a)
+    assert [p["self_check"] for p in pr] == [True, True] and line["self_check"] is True
+    assert line["distributed"]["backend"] == "gloo"
+    assert line["distributed"]["device_identity"]["distinct"] is True
+
+
+def test_a_failing_rank_check_fails_the_line():
+    r = _run(["--gpus", "3", "--launch-check", "--requests", "1010"], MIRSHA_BENCH_CHECK_CORRUPT_RANK="2")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert [p["self_check"] for p in line["per_rank"]] == [True, True, False]
+    assert line["self_check"] is False
 
 
 def test_gpus_3_self_launches_three_ranks():
