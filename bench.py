@@ -948,7 +948,7 @@ def config3_leg(a, eng, dev):
         tops = work_blocks * OPS_PER_COMPRESSION / (ms_k / steps * 1e-3) / 1e12
         tkey = kernel_source_key(a.variant)
         traffic, _ = lookup_traffic(a.traffic_file, tkey, 3, kname)
-        step_tops = (wl.req_blocks + wl.bat_blocks) * OPS_PER_COMPRESSION / (dt / steps * 1e-3) / 1e12
+        step_tops = (wl.req_blocks + wl.bat_blocks) * OPS_PER_COMPRESSION / (dt / steps) / 1e12
         leg = {"plan": wl.plan.mode_name, "ms_per_step": dt / steps * 1e3,
                "digests_per_s": wl.digests * steps / dt, "kernel": kname, "avg_launch_ms": kms,
                "frac": tops / VALU_PEAK_TOPS, "step_frac": step_tops / VALU_PEAK_TOPS,
