@@ -225,7 +225,10 @@ void parallel_for(uint32_t n, int threads, const std::function<void(uint32_t, ui
 }
 
 uint64_t exclusive_scan(const uint32_t* len, uint32_t n, uint64_t* out) {
-    const int T = n < (1u << 16) ? 1 : std::min<int>(max_threads(), (int)(n >> 15));
+    // The caller's share of the host threads, as threads_for: a mirsha_multi
+    // worker (pool slot set) gets its own slice of them.
+    const int budget = t_pool_slot ? std::max(t_pool_threads, 1) : max_threads();
+    const int T = n < (1u << 16) ? 1 : std::min<int>(budget, (int)(n >> 15));
     if (T <= 1) {
         uint64_t p = 0;
         for (uint32_t i = 0; i < n; i++) {

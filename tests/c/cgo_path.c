@@ -32,7 +32,9 @@
  * tests/test_c_abi.py to compare with the oracle; every leg's digests are
  * compared with the serial leg's.  Exit 0 = ok.
  *
- * Usage: cgo_path [n] [data_len] [threads] [reps] [chunk_mib] [pack_stores: plain|nt]
+ * Usage: cgo_path [n] [data_len] [threads] [reps] [chunk_mib] [pack_stores: plain|nt] [big_every big_len]
+ * (big_every > 0: every big_every-th request carries big_len payload bytes;
+ * "sample_big" then holds the first such request's digest)
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
@@ -310,10 +312,15 @@ static void len_part(void* arg, int part, int parts) {
 static uint64_t lengths_parallel(const Request* reqs, uint32_t n, uint32_t* lens, Pool* pool, LenJob* j) {
     j->reqs = reqs;
     j->n = n;
-    j->br = (n + MAX_BLOCKS - 1) / MAX_BLOCKS;
-    j->nb = (n + j->br - 1) / j->br;
     j->lens = lens;
     j->bpre[0] = 0;
+    if (n == 0) { /* no blocks (and no division by a zero block size) */
+        j->br = 1;
+        j->nb = 0;
+        return 0;
+    }
+    j->br = (n + MAX_BLOCKS - 1) / MAX_BLOCKS;
+    j->nb = (n + j->br - 1) / j->br;
     pool_run(pool, len_part, j);
     for (uint32_t k = 0; k < j->nb; k++) j->bpre[k + 1] += j->bpre[k];
     return j->bpre[j->nb];
@@ -342,7 +349,7 @@ static void hash_batch_onecall(const Request* reqs, uint32_t n, uint8_t* arena, 
  * and D2H are queued), so neither the submission's host work nor the DMA
  * waits for packing.  {pack ms = until the last submission returned, call ms
  * = wait + the last digests}.  *chunks_out = submissions. */
-#define MAX_CHUNKS 4096
+#define MAX_CHUNKS 65536
 /* host phases of the last chunked call (ms): offsets, waiting for the packing
  * workers, submits (overlapping the packing), final wait, final copy */
 static double ph_off, ph_pack, ph_submit, ph_wait, ph_copy;
@@ -363,36 +370,66 @@ static void submit_chunk(mirsha_multi* m, const uint8_t* arena, uint64_t total, 
 static void hash_batch_chunked(const Request* reqs, uint32_t n, uint8_t* arena, uint64_t* off, uint32_t* lens,
                                uint8_t* dig_pinned, uint8_t* dig, Pool* pool, uint64_t chunk_bytes, mirsha_multi* m,
                                double* pack_ms, double* call_ms, int* chunks_out) {
-    static uint64_t ticket[MAX_CHUNKS];
-    static uint32_t cfirst[MAX_CHUNKS + 1], cblk[MAX_CHUNKS + 1];
+    static uint64_t ticket[MAX_CHUNKS], cat[MAX_CHUNKS];
+    static uint32_t cfirst[MAX_CHUNKS + 1], cb0[MAX_CHUNKS], cb1[MAX_CHUNKS];
     static LenJob lj;
     const double t0 = now_ms();
     const uint64_t total = lengths_parallel(reqs, n, lens, pool, &lj);
     ph_off = now_ms() - t0;
     ph_pack = ph_submit = ph_max_submit = ph_max_pool = 0.0;
-    /* chunk boundaries at block granularity: blocks [b0, b1) until the
-     * chunk's bytes reach the budget -- a quarter, a half, then whole budgets:
-     * the link starts early and stays busy while the workers pack the next,
-     * larger chunk */
+    /* Chunk boundaries (INTEGRATION.md planChunks): whole blocks [b0, b1)
+     * until the chunk's bytes reach the budget -- a quarter, a half, then whole
+     * budgets: the link starts early and stays busy while the workers pack the
+     * next, larger chunk.  A block holding more than a whole budget (large
+     * messages) is cut at request boundaries instead -- chunk k is then
+     * requests [cfirst[k], cfirst[k+1]) of one block, starting at byte cat[k],
+     * cb0[k] == cb1[k] -- so no submission outgrows one device arena
+     * (MIRSHA_MAX_DEVICE_ARENA_BYTES). */
     int nk = 0;
     for (uint32_t b0 = 0; b0 < lj.nb;) {
         const uint64_t budget = nk == 0 ? chunk_bytes / 4 : nk == 1 ? chunk_bytes / 2 : chunk_bytes;
+        const uint32_t r0 = b0 * lj.br, r1 = r0 + lj.br < n ? r0 + lj.br : n;
+        if (lj.bpre[b0 + 1] - lj.bpre[b0] > chunk_bytes) {
+            uint64_t at = lj.bpre[b0];
+            for (uint32_t lo = r0; lo < r1;) {
+                uint32_t hi = lo + 1;
+                uint64_t s = lens[lo];
+                while (hi < r1 && s + lens[hi] <= chunk_bytes) s += lens[hi++];
+                if (nk == MAX_CHUNKS) exit(6);
+                cfirst[nk] = lo;
+                cb0[nk] = cb1[nk] = b0;
+                cat[nk++] = at;
+                at += s;
+                lo = hi;
+            }
+            b0++;
+            continue;
+        }
         uint32_t b1 = b0 + 1;
-        while (b1 < lj.nb && lj.bpre[b1] - lj.bpre[b0] < budget) b1++;
+        while (b1 < lj.nb && lj.bpre[b1] - lj.bpre[b0] < budget && lj.bpre[b1 + 1] - lj.bpre[b1] <= chunk_bytes) b1++;
         if (nk == MAX_CHUNKS) exit(6);
-        cblk[nk] = b0;
-        cfirst[nk++] = b0 * lj.br;
+        cfirst[nk] = r0;
+        cb0[nk] = b0;
+        cb1[nk] = b1;
+        cat[nk++] = lj.bpre[b0];
         b0 = b1;
     }
-    cblk[nk] = lj.nb;
     cfirst[nk] = n;
     int copied = 0; /* chunks whose digests are in dig */
     ChunkJob job;
     for (int k = 0; k <= nk; k++) {
         /* workers: pack chunk k (if any) + the digests of chunks already back */
         const double tp = now_ms();
+        const int part_block = k < nk && cb0[k] == cb1[k];
         job = (ChunkJob){reqs, arena, off, k < nk ? cfirst[k] : 0, k < nk ? cfirst[k + 1] : 0, dig_pinned, dig, 0, 0,
-                         lj.bpre, lens, n, lj.br, k < nk ? cblk[k] : 0, k < nk ? cblk[k + 1] : 0};
+                         part_block ? NULL : lj.bpre, lens, n, lj.br, k < nk ? cb0[k] : 0, k < nk ? cb1[k] : 0};
+        if (part_block) { /* a part of one oversized block: its few offsets here, the workers split its requests */
+            uint64_t p = cat[k];
+            for (uint32_t i = cfirst[k]; i < cfirst[k + 1]; i++) {
+                off[i] = p;
+                p += lens[i];
+            }
+        }
         int upto = copied;
         while (upto < k - 1) {
             int done = 0;
@@ -486,6 +523,10 @@ int main(int argc, char** argv) {
     const int reps = argc > 4 ? atoi(argv[4]) : 5;
     const double chunk_mib = argc > 5 ? atof(argv[5]) : 16.0;
     g_nt = argc > 6 && strcmp(argv[6], "nt") == 0;
+    /* optional large messages: request i with i % big_every == big_every - 1
+     * carries big_len payload bytes (its block then outgrows a chunk budget) */
+    const uint32_t big_every = argc > 7 ? (uint32_t)strtoul(argv[7], NULL, 10) : 0u;
+    const uint32_t big_len = argc > 8 ? (uint32_t)strtoul(argv[8], NULL, 10) : 0u;
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
     if (n < 4 || reps < 1 || reps > 64 || chunk_mib <= 0) return 5;
@@ -503,20 +544,21 @@ int main(int argc, char** argv) {
     Request* reqs = malloc(sizeof(Request) * n);
     uint64_t total = 0;
     for (uint32_t i = 0; i < n; i++) {
+        const uint32_t dl = big_every && i % big_every == big_every - 1 ? big_len : data_len;
         uint8_t* h0 = malloc(8);
         uint8_t* h1 = malloc(8);
-        uint8_t* d = malloc(data_len ? data_len : 1);
+        uint8_t* d = malloc(dl ? dl : 1);
         const uint64_t c = i % 16u, r = i / 16u;
         for (int b = 0; b < 8; b++) {
             h0[b] = (uint8_t)(c >> (8 * b));
             h1[b] = (uint8_t)(r >> (8 * b));
         }
-        for (uint32_t j = 0; 8u * j < data_len; j++) {
+        for (uint32_t j = 0; 8u * j < dl; j++) {
             const uint64_t v = splitmix64(splitmix64(0x6D69726266740002ull ^ i) + j);
-            for (uint32_t b = 0; b < 8 && 8u * j + b < data_len; b++) d[8u * j + b] = (uint8_t)(v >> (8 * b));
+            for (uint32_t b = 0; b < 8 && 8u * j + b < dl; b++) d[8u * j + b] = (uint8_t)(v >> (8 * b));
         }
-        reqs[i] = (Request){{h0, h1, d}, {8, 8, data_len}};
-        total += 16u + data_len;
+        reqs[i] = (Request){{h0, h1, d}, {8, 8, dl}};
+        total += 16u + dl;
     }
     void* ap = NULL;
     void* dp = NULL;
@@ -635,7 +677,13 @@ int main(int argc, char** argv) {
     leg_print("lib", &lib, reps, n, lphases);
     printf(", ");
     leg_print("multi", &mul, reps, n, mextra);
-    printf(", \"sample\": \"%s\"}\n", sample);
+    printf(", \"sample\": \"%s\"", sample);
+    if (big_every && big_every <= n) { /* the first large request's digest */
+        char bs[65];
+        for (int k = 0; k < 32; k++) sprintf(bs + 2 * k, "%02x", dig_s[32ull * (big_every - 1) + k]);
+        printf(", \"sample_big\": {\"index\": %u, \"payload_bytes\": %u, \"sha256\": \"%s\"}", big_every - 1, big_len, bs);
+    }
+    printf("}\n");
     pool_stop(&pool);
     mirsha_host_free(ap);
     mirsha_host_free(dp);

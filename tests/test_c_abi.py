@@ -74,19 +74,88 @@ def test_cgo_path_on_gpu(tmp_path, stores):
     assert line["requests"] == n and line["parallel"]["ms"] > 0 and line["pack_stores"] == stores
     # chunks end at block boundaries (blocks of ceil(n / 4096) requests); the
     # first two have a quarter and a half of the budget
-    br = -(-n // 4096)
-    nb = -(-n // br)
-    bsum = [min(br, n - b * br) * (16 + data_len) for b in range(nb)]
-    want_chunks, b0 = 0, 0
-    while b0 < nb:
-        budget = (1 << 20) >> (2 - want_chunks) if want_chunks < 2 else 1 << 20
-        acc, b1 = bsum[b0], b0 + 1
-        while b1 < nb and acc < budget:
-            acc += bsum[b1]
-            b1 += 1
-        want_chunks, b0 = want_chunks + 1, b1
-    assert line["parallel"]["chunks"] == want_chunks == line["multi"]["chunks"] > 20
+    chunks = plan_chunks(np.full(n, 16 + data_len), 1 << 20)
+    assert line["parallel"]["chunks"] == len(chunks) == line["multi"]["chunks"] > 20
+    assert all(hi > lo for lo, hi, _ in chunks)
     arena = oracle_py.gen_requests(0x6D69726266740002, 0, 4, data_len)
     stride = 16 + data_len
     want = oracle_py.hash_requests(arena, np.arange(4, dtype=np.uint64) * stride, np.full(4, stride))
     assert line["sample"].split(",") == [w.tobytes().hex() for w in want]
+
+
+def plan_chunks(lens, chunk_bytes):
+    """Python twin of HashBatch's chunk planner (INTEGRATION.md planChunks,
+    tests/c/cgo_path.c): [(first request, end request, whole blocks?)].
+    Whole blocks of ceil(n / 4096) requests until a quarter, a half, then a
+    whole budget is reached; a block over a whole budget is cut at request
+    boundaries (no submission may outgrow one device arena)."""
+    lens = np.asarray(lens, dtype=np.int64)
+    n = lens.size
+    if n == 0:
+        return []
+    br = -(-n // 4096)
+    nb = -(-n // br)
+    bpre = np.concatenate([[0], np.cumsum([lens[b * br:(b + 1) * br].sum() for b in range(nb)])])
+    out, b0 = [], 0
+    while b0 < nb:
+        budget = chunk_bytes >> (2 - len(out)) if len(out) < 2 else chunk_bytes
+        r0, r1 = b0 * br, min((b0 + 1) * br, n)
+        if bpre[b0 + 1] - bpre[b0] > chunk_bytes:
+            lo = r0
+            while lo < r1:
+                hi, s = lo + 1, lens[lo]
+                while hi < r1 and s + lens[hi] <= chunk_bytes:
+                    s += lens[hi]
+                    hi += 1
+                out.append((lo, hi, False))
+                lo = hi
+            b0 += 1
+            continue
+        b1 = b0 + 1
+        while b1 < nb and bpre[b1] - bpre[b0] < budget and bpre[b1 + 1] - bpre[b1] <= chunk_bytes:
+            b1 += 1
+        out.append((r0, min(b1 * br, n), True))
+        b0 = b1
+    return out
+
+
+def test_plan_chunks_splits_only_oversized_blocks():
+    n, big_every = 20_000, 1000
+    lens = np.full(n, 272)
+    lens[big_every - 1::big_every] = 16 + 3 * (1 << 20)
+    chunks = plan_chunks(lens, 1 << 20)
+    # contiguous, covering every request once
+    assert chunks[0][0] == 0 and chunks[-1][1] == n
+    assert all(a[1] == b[0] for a, b in zip(chunks, chunks[1:]))
+    # every chunk fits a budget unless it is one request; parts exist only for the 20 big blocks
+    for lo, hi, whole in chunks:
+        if not whole and hi - lo > 1:
+            assert lens[lo:hi].sum() <= 1 << 20
+    parts = [c for c in chunks if not c[2]]
+    assert sum(1 for lo, hi, _ in parts if hi - lo == 1 and lens[lo] > 1 << 20) == n // big_every
+    # the uniform config-2 shape never splits
+    assert all(w for _, _, w in plan_chunks(np.full(1 << 20, 272), 32 << 20))
+
+
+@pytest.mark.gpu
+def test_cgo_path_large_messages_split_blocks(tmp_path):
+    """a block holding more than a chunk budget (large messages) is
+    cut at request boundaries, so no mirsha_submit_batch outgrows one device
+    arena; every leg still agrees, and the large request's digest is the
+    oracle's."""
+    exe = build(tmp_path, PATH_SRC, "cgo_path")
+    n, data_len, big_every, big_len = 20_000, 256, 1000, 3 * (1 << 20)
+    r = subprocess.run([exe, str(n), str(data_len), "8", "1", "1", "nt", str(big_every), str(big_len)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    line = json.loads(r.stdout.splitlines()[-1])
+    lens = np.full(n, 16 + data_len)
+    lens[big_every - 1::big_every] = 16 + big_len
+    chunks = plan_chunks(lens, 1 << 20)
+    assert line["parallel"]["chunks"] == len(chunks) == line["multi"]["chunks"]
+    assert any(not w for _, _, w in chunks)
+    sb = line["sample_big"]
+    assert sb["index"] == big_every - 1
+    big = oracle_py.gen_requests(0x6D69726266740002, big_every - 1, 1, big_len)
+    want = oracle_py.hash_requests(big, np.zeros(1, np.uint64), np.full(1, 16 + big_len))
+    assert sb["sha256"] == want[0].tobytes().hex()
