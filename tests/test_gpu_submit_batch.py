@@ -63,6 +63,27 @@ def test_chunked_cycle_bit_exact(engine, pinned_arena, pinned_out, gap):
     assert np.array_equal(out, oracle_py.hash_requests(src, off, lens, threads=8))
 
 
+@pytest.mark.parametrize("n,budget", [(30_000, 256 * 1024), (4097, 64 * 1024), (100_003, 1 << 20)])
+def test_block_chunked_cycle_bit_exact(engine, n, budget):
+    """The chunks HashBatch really submits (go/gpuhash.go planChunks, ADVICE
+    r5): runs of whole blocks of ceil(n / 4096) requests, and blocks larger
+    than a whole budget cut at request boundaries (here the 300 KB messages'
+    blocks), each chunk one mirsha_submit_batch into a page-locked arena."""
+    from chunking import plan_chunks
+
+    src, off, lens = _cycle(21 + n, n, big_every=5000, big_len=300_000)
+    arena = engine.host_empty(src.size)
+    arena[:] = src
+    out = engine.host_empty(32 * n).reshape(n, 32)
+    chunks = plan_chunks(lens, budget)
+    assert chunks[-1][1] == n and any(w for *_, w in chunks)
+    if budget < 300_000:
+        assert any(not w for *_, w in chunks)  # split blocks present
+    tickets = [engine.submit_batch(arena, off[lo:hi], lens[lo:hi], out=out[lo:hi]) for lo, hi, _ in chunks]
+    engine.wait(tickets[-1])
+    assert np.array_equal(out, oracle_py.hash_requests(src, off, lens, threads=8))
+
+
 def test_empty_and_tiny_submissions(engine):
     src = np.frombuffer(b"abc", dtype=np.uint8).copy()
     t0 = engine.submit_batch(src, np.zeros(0, np.uint64), np.zeros(0, np.uint32))  # no requests
