@@ -22,14 +22,40 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
 
 
+class _BuildLock:
+    """An exclusive flock on oracle/.build.lock around the staleness check, the
+    rebuild and the dlopen: bench.py's ranks all self-check at once, and one
+    must never dlopen a library another is still writing.  No lock (and no
+    rebuild race to guard) when the directory is read-only."""
+
+    def __enter__(self):
+        import fcntl
+
+        try:
+            self.f = open(os.path.join(ORACLE_DIR, ".build.lock"), "w")
+        except OSError:
+            self.f = None
+            return self
+        fcntl.flock(self.f, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        if self.f is not None:
+            self.f.close()  # releases the flock
+
+
+def _load_fresh(so: str, src: str) -> ctypes.CDLL:
+    with _BuildLock():
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            build()
+        return ctypes.CDLL(so)
+
+
 def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    src = os.path.join(ORACLE_DIR, "sha256_oracle.c")
-    if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
-        build()
-    lib = ctypes.CDLL(ORACLE_SO)
+    lib = _load_fresh(ORACLE_SO, os.path.join(ORACLE_DIR, "sha256_oracle.c"))
     vp = ctypes.c_void_p
     lib.oracle_hash_requests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
     lib.oracle_hash_requests_mt.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int]
@@ -140,10 +166,7 @@ def load_evp() -> ctypes.CDLL:
     global _evp
     if _evp is not None:
         return _evp
-    src = os.path.join(ORACLE_DIR, "evp_loop.c")
-    if not os.path.exists(EVP_SO) or os.path.getmtime(EVP_SO) < os.path.getmtime(src):
-        build()
-    lib = ctypes.CDLL(EVP_SO)
+    lib = _load_fresh(EVP_SO, os.path.join(ORACLE_DIR, "evp_loop.c"))
     vp = ctypes.c_void_p
     lib.evp_hash_requests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_int]
     lib.evp_batch_digests.argtypes = [vp, vp, vp, ctypes.c_uint32, vp]
