@@ -512,16 +512,20 @@ class BatchWorkload:
             d = o.evp_hash_requests(arena, off, ln, threads=threads)
             o.evp_batch_digests(d, idx, first)
 
-        evp_ok = bool(np.array_equal(o.evp_hash_requests(arena[: 64 * stride], off[:64], ln[:64]),
-                                     o.hash_requests(arena[: 64 * stride], off[:64], ln[:64])))
-        de, dte = _time_cpu(evp, seconds / 4, (1,))[1]
-        openssl = {"value": de * per / dte, "unit": "digests/s", "cores": 1,
-                   "label": "OpenSSL stand-in for Go crypto/sha256",
-                   "openssl": o.evp_version(), "matches_oracle": evp_ok,
-                   "sample": f"{de} passes of the headline sample, {dte:.1f} s",
-                   "note": "BASELINE.md CPU-baseline plan: processor.go:133-143 with EVP_DigestInit_ex2 / "
-                           "EVP_DigestUpdate per HashRequest.Data slice (3 per request, state_machine.go:313-317) / "
-                           "EVP_DigestFinal_ex; batch digests one Update per RequestAck digest (oracle/evp_loop.c)"}
+        try:  # an extra leg: a missing libcrypto is reported in the line, not fatal to it
+            evp_ok = bool(np.array_equal(o.evp_hash_requests(arena[: 64 * stride], off[:64], ln[:64]),
+                                         o.hash_requests(arena[: 64 * stride], off[:64], ln[:64])))
+            de, dte = _time_cpu(evp, seconds / 4, (1,))[1]
+            openssl = {"value": de * per / dte, "unit": "digests/s", "cores": 1,
+                       "label": "OpenSSL stand-in for Go crypto/sha256",
+                       "openssl": o.evp_version(), "matches_oracle": evp_ok,
+                       "sample": f"{de} passes of the headline sample, {dte:.1f} s",
+                       "note": "BASELINE.md CPU-baseline plan: processor.go:133-143 with EVP_DigestInit_ex2 / "
+                               "EVP_DigestUpdate per HashRequest.Data slice (3 per request, "
+                               "state_machine.go:313-317) / EVP_DigestFinal_ex; batch digests one Update per "
+                               "RequestAck digest (oracle/evp_loop.c)"}
+        except Exception as e:  # noqa: BLE001
+            openssl = {"error": f"{type(e).__name__}: {e}"}
         # Pool legs on a larger sample (whole config up to 2^20 requests), so
         # per-pass thread start-up is noise; batch digests single-threaded, as
         # the state machine consumes them (processResults, state_machine.go:377-433).
@@ -545,9 +549,11 @@ class BatchWorkload:
             r = _time_cpu(pool, seconds / 3, (t,))[t]
             legs[name] = {"value": r[0] * pper / r[1], "threads": t,
                           "sample": f"{r[0]} passes x {npool} requests + {pfirst.size - 1} batch digests, {r[1]:.1f} s"}
-            re = _time_cpu(lambda th: evp(th, parena, poff, pln, pidx, pfirst), seconds / 6, (t,))[t]
-            openssl.setdefault("pool", {})[name] = {"value": re[0] * pper / re[1], "threads": t,
-                                                    "sample": f"{re[0]} passes of the pool sample, {re[1]:.1f} s"}
+            if "error" not in openssl:
+                re = _time_cpu(lambda th: evp(th, parena, poff, pln, pidx, pfirst), seconds / 6, (t,))[t]
+                openssl.setdefault("pool", {})[name] = {"value": re[0] * pper / re[1], "threads": t,
+                                                        "sample": f"{re[0]} passes of the pool sample, "
+                                                                  f"{re[1]:.1f} s"}
         return {
             "value": done1 * per / dt1, "unit": "digests/s", "cores": 1, "kind": "port",
             "sample": f"{done1} passes x ({n} requests x {stride} B + {first.size - 1} BatchSize-{bs} batch "
