@@ -216,6 +216,7 @@ struct mirsha_pipeline {
     DevBuf d_probe;
     bool trace = false;
     std::vector<uint32_t> cidx, cfirst;      // compacted lists (no null entries)
+    uint32_t uniform = 0;                    // B: identity lists of B entries (uniform_lists), else 0
     std::vector<uint32_t> order;             // request processing order
     DevBuf d_cidx, d_cfirst, d_order, d_state;
 };

@@ -78,10 +78,12 @@ constexpr uint32_t kMaxListEntries = (1u << 30) - 1u;
 hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32_t* idx, uint32_t n_entries,
                         const uint32_t* first, uint32_t n_lists, uint32_t* scratch, uint8_t* out, hipStream_t s);
 // One segment [ob, oe) of every (compacted) list chain; oe = kOpenEnd finalises all.
+// uniform = B > 0: the lists are identity lists of B entries (list k =
+// entries [k B, min(k B + B, n_entries)), cidx[e] == e); cidx / cfirst unread.
 constexpr uint32_t kOpenEnd = 0xFFFFFFFEu;
 hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                         const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
-                        uint8_t* out, hipStream_t s);
+                        uint8_t* out, hipStream_t s, uint32_t uniform = 0);
 // Whole (compacted) list chains by producer/consumer pairs, one 128-thread
 // workgroup per 64 lists; for at most kPairMaxGroups groups.
 hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,

@@ -1385,10 +1385,16 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
 // c <= ob (ob > 0) were finalised by an earlier segment and are skipped.
 // The waves raise their issue priority: they run beside the next request
 // chunk and must keep near-alone speed on their SIMD.
+// kUni (uni = B > 0): identity lists of B entries -- list k is digests
+// [k B, min(k B + B, n_entries)), the BatchSize batches over consecutive
+// requests of a plan (mirsha_plan.hip detects them) -- so bounds and indices
+// are computed, not loaded: the chain's first digest loads issue at once
+// instead of after two dependent loads (cfirst, then cidx).
+template <bool kUni>
 __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
     const uint8_t* __restrict__ digests, uint32_t n_digests, const uint32_t* __restrict__ cidx,
     uint32_t n_entries, const uint32_t* __restrict__ cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe,
-    uint32_t* __restrict__ state, uint8_t* __restrict__ out) {
+    uint32_t* __restrict__ state, uint8_t* __restrict__ out, uint32_t uni) {
     __builtin_amdgcn_s_setprio(3);
     const __amdgpu_buffer_rsrc_t drs =
         __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
@@ -1396,8 +1402,21 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
         __builtin_amdgcn_make_buffer_rsrc((void*)cidx, (short)0, (int)(4u * n_entries), 0x00020000);
     const uint32_t k = blockIdx.x * kBlockThreads + threadIdx.x;
     const bool valid = k < n_lists;
-    const uint32_t e0 = valid ? cfirst[k] : 0u;
-    const uint32_t c = valid ? cfirst[k + 1] - e0 : 0u;
+    uint32_t e0, c;
+    if constexpr (kUni) {
+        e0 = valid ? k * uni : 0u;
+        c = valid ? min(uni, n_entries - e0) : 0u;
+    } else {
+        e0 = valid ? cfirst[k] : 0u;
+        c = valid ? cfirst[k + 1] - e0 : 0u;
+    }
+    // digest index of ordinal o of this list (0 for a dead slot: never read live)
+    auto index = [&](uint32_t o, bool lv) -> uint32_t {
+        if constexpr (kUni)
+            return e0 + o;
+        else
+            return ld_u32(irs, 4u * (e0 + o), lv);
+    };
     const bool active = valid && (ob == 0u || c > ob);
     const bool fin = active && c <= oe;
     const uint32_t full_end = fin ? (c & ~1u) : oe;  // exclusive ordinal of the full blocks
@@ -1419,10 +1438,10 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
     // Same prefetch pipeline as hash_list: digests one block ahead, indices two.
     auto live = [&](uint32_t t, uint32_t slot) { return t < nblk && ob + 2u * t + slot < c; };
     uint4 cur[4];
-    uint32_t nx0 = ld_u32(irs, 4u * (e0 + ob + 2u), live(1, 0)), nx1 = ld_u32(irs, 4u * (e0 + ob + 3u), live(1, 1));
+    uint32_t nx0 = index(ob + 2u, live(1, 0)), nx1 = index(ob + 3u, live(1, 1));
     {
-        const uint32_t i0 = ld_u32(irs, 4u * (e0 + ob), live(0, 0));
-        const uint32_t i1 = ld_u32(irs, 4u * (e0 + ob + 1u), live(0, 1));
+        const uint32_t i0 = index(ob, live(0, 0));
+        const uint32_t i1 = index(ob + 1u, live(0, 1));
         load_digest(drs, i0, live(0, 0), cur[0], cur[1]);
         load_digest(drs, i1, live(0, 1), cur[2], cur[3]);
     }
@@ -1430,8 +1449,8 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
         uint4 nxt[4];
         load_digest(drs, nx0, live(t + 1, 0), nxt[0], nxt[1]);
         load_digest(drs, nx1, live(t + 1, 1), nxt[2], nxt[3]);
-        const uint32_t nn0 = ld_u32(irs, 4u * (e0 + ob + 2u * t + 4u), live(t + 2, 0));
-        const uint32_t nn1 = ld_u32(irs, 4u * (e0 + ob + 2u * t + 5u), live(t + 2, 1));
+        const uint32_t nn0 = index(ob + 2u * t + 4u, live(t + 2, 0));
+        const uint32_t nn1 = index(ob + 2u * t + 5u, live(t + 2, 1));
         if (t < nblk) {
             uint32_t w[16];
 #pragma unroll
@@ -2272,11 +2291,19 @@ hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32
 
 hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                         const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
-                        uint8_t* out, hipStream_t s) {
+                        uint8_t* out, hipStream_t s, uint32_t uniform) {
     if (n_lists == 0) return hipSuccess;
     const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
-    sha256_chain_kernel<<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists, ob, oe,
-                                                      state, out);
+    if (uniform) {
+        // identity lists: list k = entries [k B, ...) must lie inside n_entries
+        if ((uint64_t)(n_lists - 1u) * uniform >= n_entries || (uint64_t)n_lists * uniform < n_entries)
+            return hipErrorInvalidValue;
+        sha256_chain_kernel<true><<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists,
+                                                                 ob, oe, state, out, uniform);
+    } else {
+        sha256_chain_kernel<false><<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst,
+                                                                  n_lists, ob, oe, state, out, 0u);
+    }
     return hipGetLastError();
 }
 

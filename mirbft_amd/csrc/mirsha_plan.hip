@@ -15,6 +15,26 @@ namespace mirsha_api {
 // Stream-level pipelining (chain segments on a second stream) and the
 // in-kernel continuation form were measured slower at BASELINE sizes and
 // removed (code in git history before round 2).
+// B when the compacted lists are identity lists of B entries -- list k is
+// entries [k B, min(k B + B, n)) and cidx[e] == e: BatchSize batches over
+// consecutive requests (sequence.go:154-157 as the synthetic streams and the
+// bench build them) -- else 0.  The chain kernel then computes bounds and
+// indices instead of loading them (sha256_chain_kernel<true>).
+uint32_t uniform_lists(const std::vector<uint32_t>& cidx, const std::vector<uint32_t>& cfirst) {
+    const size_t n_lists = cfirst.size() - 1, n = cidx.size();
+    if (n_lists == 0 || n == 0 || cfirst[1] == 0) return 0;
+    const uint64_t B = cfirst[1];
+    if ((n_lists - 1) * B >= n || n_lists * B < n) return 0;
+    for (size_t k = 0; k < n_lists; k++)
+        if (cfirst[k] != k * B) return 0;
+    for (size_t e = 0; e < n; e++)
+        if (cidx[e] != e) return 0;
+    // A/B (MIRSHA_AB=1 MIRSHA_CHAIN_UNIFORM=0): the loaded-index form
+    if (const char* e = mirsha::ab_getenv("MIRSHA_CHAIN_UNIFORM"))
+        if (e[0] == '0') return 0;
+    return (uint32_t)B;
+}
+
 int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint32_t* idx, const uint32_t* first,
                    uint32_t n_lists, const uint32_t* len) {
     p->n_req = n_req;
@@ -32,6 +52,7 @@ int pipeline_build(mirsha_ctx* c, mirsha_pipeline* p, uint32_t n_req, const uint
         p->cfirst[k + 1] = (uint32_t)p->cidx.size();
     }
     p->n_entries = (uint32_t)p->cidx.size();
+    p->uniform = uniform_lists(p->cidx, p->cfirst);
     // Processing order: listed requests first, then longest-first by block
     // count (length bucketing inside a wave), stable.
     p->order.resize(n_req);
@@ -74,7 +95,7 @@ int pipeline_run(mirsha_ctx* c, mirsha_pipeline* p, const uint8_t* d_arena, uint
     return timed_launch(c, 1, [&] {
         return mirsha::launch_chain(d_req_out, p->n_req, p->d_cidx.as<uint32_t>(), p->n_entries,
                                     p->d_cfirst.as<uint32_t>(), p->n_lists, 0u, mirsha::kOpenEnd,
-                                    p->d_state.as<uint32_t>(), d_list_out, c->stream);
+                                    p->d_state.as<uint32_t>(), d_list_out, c->stream, p->uniform);
     });
 }
 

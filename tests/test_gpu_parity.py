@@ -585,6 +585,47 @@ def test_pipeline_overlap_irregular_lists(engine):
     plan.close()
 
 
+def _lists(kind, n, bs, rng):
+    """(idx, first): identity BatchSize lists (the chain kernel's computed-index
+    form) and near misses that must take the loaded-index form."""
+    idx, first = sharding.batch_lists(n, bs)
+    idx, first = idx.copy(), first.astype(np.int64)
+    if kind == "permuted":  # uniform bounds, entries not the identity
+        idx = rng.permutation(n).astype(np.uint32)
+    elif kind == "short_middle" and first.size > 3:  # identity entries, one list cut short in the middle
+        first = np.delete(first, 1)
+        first = np.insert(first, 1, max(bs // 2, 1))
+        first = np.maximum.accumulate(first)
+    elif kind == "offset":  # identity lists not starting at request 0
+        idx = idx[1:]
+        first = np.minimum(first, idx.size)
+    return idx.astype(np.uint32), first.astype(np.uint32)
+
+
+@pytest.mark.parametrize("kind", ["identity", "permuted", "short_middle", "offset"])
+# more than kPairMaxGroups x 64 = 32,768 lists: the chain kernel (fewer go to the pair kernel)
+@pytest.mark.parametrize("n,bs", [(40_000, 1), (70_001, 2), (245_763, 7), (700_003, 20)])
+def test_pipeline_uniform_lists(engine, kind, n, bs):
+    """Sequential plans over BatchSize lists: identity lists of one size run the
+    chain kernel's computed-index form (round 6: no cfirst / cidx loads), every
+    near miss the loaded-index form; both bit-exact vs the oracle, the final
+    (short) list included."""
+    rng = np.random.default_rng(n + bs)
+    lens = rng.integers(0, 300, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(lens[:-1], out=off[1:])
+    arena = rng.integers(0, 256, int(lens.sum()) + 1, dtype=np.uint8)
+    idx, first = _lists(kind, n, bs, rng)
+    plan = engine.pipeline(n, idx, first, lens, mode="sequential")
+    assert plan.mode_name == "sequential"
+    want_req = oracle_py.hash_requests(arena, off, lens)
+    want_lst = oracle_py.batch_digests(want_req, idx, first)
+    for req, lst in _plan_run(engine, plan, arena, off, lens, first.size - 1, runs=2):
+        assert np.array_equal(req, want_req)
+        assert np.array_equal(lst, want_lst)
+    plan.close()
+
+
 def _irregular(seed, n=3000, n_lists=300, max_list=60, max_len=600, min_len=0):
     rng = np.random.default_rng(seed)
     lens = rng.integers(min_len, max_len, n).astype(np.uint32)
