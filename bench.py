@@ -132,6 +132,11 @@ def parse():
     p.add_argument("--events-in-timed-loop", type=int, default=1,
                    help="1: per-kernel HIP events inside the timed loop (roofline from the same region); "
                         "0: time the loop bare, then measure kernels in a second identical pass")
+    p.add_argument("--event-every", type=int, default=4,
+                   help="inside the timed loop the dominant kernel's HIP events ride on every k-th step's launch "
+                        "(bound to its dispatch, hipExtLaunchKernel): an event-bound launch adds ~5 us of stream "
+                        "time on gfx950 (profiles/r06h), so the wall time carries 1/k of it; the kernel average "
+                        "is over the sampled launches of the same timed region")
     return p.parse_args()
 
 
@@ -582,9 +587,9 @@ class BatchWorkload:
         ONE launch per cycle hashes the cycle's requests and the previous
         cycle's batches, as a stream of Ready() cycles pipelines (the state
         machine batches digests of earlier cycles).  Measured after the
-        headline steps on rank 0: --steps launches with the kernel's HIP
-        events on, wall time and kernel time from that ONE pass (kernel <=
-        wall holds by construction)."""
+        headline steps on rank 0: --steps launches, the kernel's HIP events
+        on every k-th one (--event-every), wall time and kernel time from that
+        ONE pass (kernel <= wall holds by construction)."""
         if self.plan is None or self.overlap:
             return None
         timer = KERNEL_FUSED if self.plan.mode_name == "fused" else KERNEL_OVERLAP
@@ -606,8 +611,10 @@ class BatchWorkload:
         e.set_timing_mask([timer])
         e.set_timing(True)
         e.reset_timing()
+        every = max(1, self.a.event_every)
         t0 = time.perf_counter()
-        for _ in range(steps):
+        for i in range(steps):
+            e.set_timing(i % every == 0)  # events ride on every k-th launch (see --event-every)
             launch()
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
@@ -624,7 +631,7 @@ class BatchWorkload:
                 "note": "one launch per cycle: this cycle's requests + the previous cycle's batch chains "
                         "(mirsha_pipeline_overlap_device, on this plan), steady state of a cycle stream; "
                         "frac = both over the kernel's event time, step_frac = both over ms_per_step; "
-                        "one pass, events on"}
+                        "one pass: wall time and the events of every k-th launch (--event-every)"}
 
     def extra(self):
         mode = self.plan.mode_name if self.plan is not None else "none"
@@ -1218,14 +1225,16 @@ def main():
     if dist:
         dist.barrier()
 
-    def timed(with_events):
+    def timed(with_events, every=1):
         eng.set_timing(with_events)
         eng.reset_timing()
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        for _ in range(a.steps):
+        for i in range(a.steps):
+            if with_events and every > 1:
+                eng.set_timing(i % every == 0)  # events on every k-th step's launch only
             wl.step()
         torch.cuda.synchronize(dev)
         if dist:
@@ -1236,7 +1245,9 @@ def main():
 
     if a.timed_kernels == "dominant":
         eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED, KERNEL_OVERLAP])
-    dt = timed(bool(a.events_in_timed_loop))
+    every = max(1, a.event_every) if a.events_in_timed_loop else 1
+    dt = timed(bool(a.events_in_timed_loop), every)
+    ev_steps = len(range(0, a.steps, every))  # steps whose dominant launches carry events
     if not a.events_in_timed_loop:
         timed(True)
     wl.after()
@@ -1286,7 +1297,7 @@ def main():
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     value = float(tot[0].item()) * a.steps / dt
     gbps = float(tot[1].item()) * a.steps / dt / 1e9
-    ms_per_step_k = ms_k / a.steps  # all launches of the dominant kernel in one step
+    ms_per_step_k = ms_k / ev_steps  # all launches of the dominant kernel in one (sampled) step
     achieved_tops = work_blocks * OPS_PER_COMPRESSION / (ms_per_step_k * 1e-3) / 1e12
     hbm_gbs = hbm_bytes / (ms_per_step_k * 1e-3) / 1e9
     # per-GPU average over the whole step's wall time (max over ranks)
@@ -1370,10 +1381,11 @@ def main():
                 "traffic": traffic,
                 "kernel": kname,
                 "avg_launch_ms": ms_k / max(n_k, 1),
-                "launches_per_step": n_k / a.steps,
+                "launches_per_step": n_k / ev_steps,
+                "timed_launches": n_k,
                 "kernel_ms_per_step": ms_per_step_k,
                 "work": f"{work_blocks} compressions x {OPS_PER_COMPRESSION} int32 ops per step "
-                        f"(over {n_k // a.steps} launch(es))",
+                        f"(over {n_k // ev_steps} launch(es))",
                 "hbm_algorithmic_gb_per_s": hbm_gbs,
                 "hbm_frac": hbm_gbs / HBM_PEAK_GBS,
                 "traffic_key": tkey,
@@ -1388,6 +1400,7 @@ def main():
             "effective_clock_ghz": probe["clock_ghz"] if probe else None,
             **wl.extra(),
             "events_in_timed_loop": bool(a.events_in_timed_loop),
+            "event_every": every,
             "timed_kernels": a.timed_kernels,
             "self_check": check_all,
             "self_check_scope": "every rank: its own range's first and last batch-aligned windows (the final "

@@ -238,19 +238,26 @@ hipEvent_t take_event(KernelTimer& t);
 // Brackets one launch with events on the launch stream when timing is on.
 template <class F>
 int timed_launch_on(mirsha_ctx* c, int which, hipStream_t st, F&& launch) {
+    // The events ride on the kernel's own dispatch (mirsha::launch_k,
+    // hipExtLaunchKernel): its start and end timestamps, no marker packets.
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->timing && ((c->time_mask >> which) & 1u);
     if (timed) {
         e0 = take_event(c->timers[which]);
         e1 = take_event(c->timers[which]);
-        if (e0) (void)hipEventRecord(e0, st);
+        if (e0 && e1) mirsha::next_launch_events() = {e0, e1};
     }
+    (void)st;
     hipError_t e = launch();
-    if (e != hipSuccess) return fail(c, MIRSHA_EHIP, "kernel launch: %s", hipGetErrorString(e));
-    if (timed && e0 && e1) {
-        (void)hipEventRecord(e1, st);
-        c->timers[which].pending.emplace_back(e0, e1);
+    // unconsumed: the launch function launched nothing (an empty call)
+    const bool bound = e0 && e1 && !mirsha::next_launch_events().start;
+    mirsha::next_launch_events() = {};
+    if (timed && (!bound || e != hipSuccess)) {
+        if (e0) c->timers[which].pool.push_back(e0);
+        if (e1) c->timers[which].pool.push_back(e1);
     }
+    if (e != hipSuccess) return fail(c, MIRSHA_EHIP, "kernel launch: %s", hipGetErrorString(e));
+    if (bound) c->timers[which].pending.emplace_back(e0, e1);
     return MIRSHA_OK;
 }
 

@@ -67,6 +67,16 @@ constexpr uint32_t kMaxBufferMsgs = 1u << 27;
 // tmp == nullptr only sets tmp_bytes (the scratch size for n requests).
 hipError_t launch_offsets_scan(void* tmp, size_t& tmp_bytes, const uint32_t* len, uint64_t* off, uint32_t n,
                                hipStream_t s);
+// Timing events for the next kernel this thread launches (timed_launch_on):
+// bound to that kernel's own dispatch through hipExtLaunchKernel, so they
+// carry its start and end timestamps and add no marker packets to the stream
+// (separate hipEventRecord markers around each launch cost ~2.7 us of stream
+// time apiece on gfx950, profiles/r06g).  Consumed (reset) by the launch.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents& next_launch_events();
+
 hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
                        const uint32_t* len, const uint32_t* order, uint32_t n, uint8_t* out,
                        int variant, hipStream_t s);

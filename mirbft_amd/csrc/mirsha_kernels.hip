@@ -21,6 +21,8 @@
 #include <cstdlib>
 #include <cstdio>
 
+#include <hip/hip_ext.h>
+
 #include "mirsha_kernels.h"
 #include "sha256_device.h"
 
@@ -2124,6 +2126,28 @@ __global__ void gen_mixed_kernel(uint64_t seed, uint64_t first, uint64_t count, 
     }
 }
 
+// ---- launching ------------------------------------------------------------
+LaunchEvents& next_launch_events() {
+    thread_local LaunchEvents ev;
+    return ev;
+}
+
+// Every kernel of the library is launched here: with the thread's pending
+// timing events bound to the dispatch (hipExtLaunchKernel) when a timed
+// launch set them, else a plain launch.  Errors are left for the caller's
+// hipGetLastError, as with <<<...>>>.
+template <typename... P, typename... A>
+void launch_k(void (*k)(P...), dim3 grid, dim3 block, uint32_t shmem, hipStream_t s, A... args) {
+    LaunchEvents& ev = next_launch_events();
+    if (ev.start && ev.stop) {
+        const hipEvent_t e0 = ev.start, e1 = ev.stop;
+        ev = LaunchEvents{};
+        hipExtLaunchKernelGGL(k, grid, block, shmem, s, e0, e1, 0u, static_cast<P>(args)...);
+    } else {
+        k<<<grid, block, shmem, s>>>(static_cast<P>(args)...);
+    }
+}
+
 // ---- clock probe (bench diagnostics; no digest depends on it) ---------------
 // Every SIMD runs kProbeWavesPerSimd waves of back-to-back throughput-form
 // compressions on registers (the request kernel's rounds, no memory traffic);
@@ -2156,11 +2180,12 @@ __global__ __launch_bounds__(256) void clock_probe_kernel(uint32_t iters, unsign
 
 hipError_t launch_clock_probe(uint32_t blocks, uint32_t iters, unsigned long long* stamps, uint32_t* sink,
                               hipStream_t s) {
-    clock_probe_kernel<<<blocks, 256, 0, s>>>(iters, stamps, sink);
+    launch_k(clock_probe_kernel, blocks, 256, 0, s, iters, stamps, sink);
     return hipGetLastError();
 }
 
 // ---- host-side launchers --------------------------------------------------
+
 const char* ab_getenv(const char* name) {
     const char* ab = getenv("MIRSHA_AB");
     return (ab && ab[0] == '1') ? getenv(name) : nullptr;
@@ -2219,15 +2244,15 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
     const uint32_t grid = (tiles + kWavesPerBlock - 1u) / kWavesPerBlock;
     const uint32_t mgrid = (tiles + kMsgWaves - 1u) / kMsgWaves;
     if (arena_len > kMaxBufferArena || n >= kMaxBufferMsgs) {  // 64-bit addressing (LDS loader)
-        sha256_msgs_kernel<true, true><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        launch_k(sha256_msgs_kernel<true, true>, mgrid, 64 * kMsgWaves, 0, s, arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantPair || (variant == kVariantLds && tiles <= pair_max_groups())) {
-        sha256_msgs_pair_kernel<<<tiles, kPairThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        launch_k(sha256_msgs_pair_kernel, tiles, kPairThreads, 0, s, arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantLowOcc || (variant == kVariantLds && tiles <= kLowOccTiles)) {
-        sha256_msgs_lowocc_kernel<<<grid, kBlockThreads, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        launch_k(sha256_msgs_lowocc_kernel, grid, kBlockThreads, 0, s, arena, arena_len, off, len, order, n, out);
         return hipGetLastError();
     }
     if (variant == kVariantCu || variant_is_ab_form(variant) ||
@@ -2247,27 +2272,27 @@ hipError_t launch_msgs(const uint8_t* arena, uint64_t arena_len, const uint64_t*
         const int slots[6] = {0, 1, 2, 5, 6, 7};  // dyn_lds_attr forms (3: fused, 4: placement probe)
         if (hipError_t e = dyn_lds_attr(fns[form], slots[form], kCuLds)) return e;
         if (form == 4)
-            sha256_msgs_cu_kernel<4><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            launch_k(sha256_msgs_cu_kernel<4>, cgrid, 64u * wg_waves, kCuLds, s, arena, arena_len, off, len, order, n, out);
         else if (form == 5)
-            sha256_msgs_cu_kernel<5><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            launch_k(sha256_msgs_cu_kernel<5>, cgrid, 64u * wg_waves, kCuLds, s, arena, arena_len, off, len, order, n, out);
         else if (form == 1)
-            sha256_msgs_cu_kernel<1><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            launch_k(sha256_msgs_cu_kernel<1>, cgrid, 64u * wg_waves, kCuLds, s, arena, arena_len, off, len, order, n, out);
         else if (form == 2)
-            sha256_msgs_cu_kernel<2><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            launch_k(sha256_msgs_cu_kernel<2>, cgrid, 64u * wg_waves, kCuLds, s, arena, arena_len, off, len, order, n, out);
         else if (form == 3)
-            sha256_msgs_cu_kernel<3><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            launch_k(sha256_msgs_cu_kernel<3>, cgrid, 64u * wg_waves, kCuLds, s, arena, arena_len, off, len, order, n, out);
         else
 #endif
         {
             if (hipError_t e = dyn_lds_attr((const void*)sha256_msgs_cu_kernel<0>, 0, kCuLds)) return e;
-            sha256_msgs_cu_kernel<0><<<cgrid, 64u * wg_waves, kCuLds, s>>>(arena, arena_len, off, len, order, n, out);
+            launch_k(sha256_msgs_cu_kernel<0>, cgrid, 64u * wg_waves, kCuLds, s, arena, arena_len, off, len, order, n, out);
         }
         return hipGetLastError();
     }
     if (variant == kVariantDirect)
-        sha256_msgs_kernel<false><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        launch_k(sha256_msgs_kernel<false>, mgrid, 64 * kMsgWaves, 0, s, arena, arena_len, off, len, order, n, out);
     else
-        sha256_msgs_kernel<true><<<mgrid, 64 * kMsgWaves, 0, s>>>(arena, arena_len, off, len, order, n, out);
+        launch_k(sha256_msgs_kernel<true>, mgrid, 64 * kMsgWaves, 0, s, arena, arena_len, off, len, order, n, out);
     return hipGetLastError();
 }
 
@@ -2276,7 +2301,7 @@ hipError_t launch_msgs_overlap(const OverlapArgs& a, hipStream_t s) {
     if (a.list_waves + tiles == 0) return hipSuccess;
     if (a.arena_len > kMaxBufferArena || a.n_req >= kMaxBufferMsgs || (a.list_waves && a.n_lists == 0))
         return hipErrorInvalidValue;
-    sha256_msgs_overlap_kernel<<<a.list_waves + tiles, 64, 0, s>>>(a);
+    launch_k(sha256_msgs_overlap_kernel, a.list_waves + tiles, 64, 0, s, a);
     return hipGetLastError();
 }
 
@@ -2284,7 +2309,7 @@ hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32
                         const uint32_t* first, uint32_t n_lists, uint32_t* scratch, uint8_t* out, hipStream_t s) {
     if (n_lists == 0) return hipSuccess;
     const uint32_t grid = (n_lists + kBlockThreads - 1u) / kBlockThreads;
-    sha256_lists_kernel<<<grid, kBlockThreads, 0, s>>>(digests, n_digests, idx, n_entries, first, n_lists, scratch,
+    launch_k(sha256_lists_kernel, grid, kBlockThreads, 0, s, digests, n_digests, idx, n_entries, first, n_lists, scratch,
                                                       out);
     return hipGetLastError();
 }
@@ -2298,10 +2323,10 @@ hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32
         // identity lists: list k = entries [k B, ...) must lie inside n_entries
         if ((uint64_t)(n_lists - 1u) * uniform >= n_entries || (uint64_t)n_lists * uniform < n_entries)
             return hipErrorInvalidValue;
-        sha256_chain_kernel<true><<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists,
+        launch_k(sha256_chain_kernel<true>, grid, kBlockThreads, 0, s, digests, n_digests, cidx, n_entries, cfirst, n_lists,
                                                                  ob, oe, state, out, uniform);
     } else {
-        sha256_chain_kernel<false><<<grid, kBlockThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst,
+        launch_k(sha256_chain_kernel<false>, grid, kBlockThreads, 0, s, digests, n_digests, cidx, n_entries, cfirst,
                                                                   n_lists, ob, oe, state, out, 0u);
     }
     return hipGetLastError();
@@ -2311,7 +2336,7 @@ hipError_t launch_chain_pair(const uint8_t* digests, uint32_t n_digests, const u
                              const uint32_t* cfirst, uint32_t n_lists, uint8_t* out, hipStream_t s) {
     if (n_lists == 0) return hipSuccess;
     const uint32_t groups = (n_lists + 63u) / 64u;
-    sha256_chain_pair_kernel<<<groups, kPairThreads, 0, s>>>(digests, n_digests, cidx, n_entries, cfirst, n_lists, out);
+    launch_k(sha256_chain_pair_kernel, groups, kPairThreads, 0, s, digests, n_digests, cidx, n_entries, cfirst, n_lists, out);
     return hipGetLastError();
 }
 
@@ -2319,7 +2344,7 @@ hipError_t launch_fused_paced(const FusedArgs& a, uint32_t grid, uint32_t pace, 
     if (grid == 0) return hipSuccess;
     if (pace < 1 || pace > kPacedMaxPace || a.n_queues != pace) return hipErrorInvalidValue;
     if (hipError_t e = dyn_lds_attr((const void*)sha256_fused_paced_kernel, 3, kPacedLds)) return e;
-    sha256_fused_paced_kernel<<<grid, 256u * pace, kPacedLds, s>>>(a);
+    launch_k(sha256_fused_paced_kernel, grid, 256u * pace, kPacedLds, s, a);
     return hipGetLastError();
 }
 
@@ -2327,13 +2352,13 @@ hipError_t launch_placement_probe(uint32_t grid, uint32_t pace, uint32_t* broken
     if (grid == 0) return hipSuccess;
     if (pace < 1 || pace > kPacedMaxPace) return hipErrorInvalidValue;
     if (hipError_t e = dyn_lds_attr((const void*)placement_probe_kernel, 4, kPacedLds)) return e;
-    placement_probe_kernel<<<grid, 256u * pace, kPacedLds, s>>>(broken, test);
+    launch_k(placement_probe_kernel, grid, 256u * pace, kPacedLds, s, broken, test);
     return hipGetLastError();
 }
 
 hipError_t launch_mixed_lengths(uint64_t seed, uint64_t first, uint64_t count, uint32_t* len, hipStream_t s) {
     if (count == 0) return hipSuccess;
-    mixed_lengths_kernel<<<(unsigned)((count + 255u) / 256u), 256, 0, s>>>(seed, first, count, len);
+    launch_k(mixed_lengths_kernel, (unsigned)((count + 255u) / 256u), 256, 0, s, seed, first, count, len);
     return hipGetLastError();
 }
 
@@ -2454,7 +2479,7 @@ __global__ __launch_bounds__(kBlockThreads) void chains_reset_kernel(const uint3
 hipError_t launch_chains_absorb(const uint8_t* digests, const uint32_t* pos, const uint32_t* act, const uint32_t* afirst,
                                 uint32_t n_active, uint32_t* h, uint32_t* pend, uint64_t* cnt, hipStream_t s) {
     if (n_active == 0) return hipSuccess;
-    chains_absorb_kernel<<<(n_active + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s>>>(
+    launch_k(chains_absorb_kernel, (n_active + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s, 
         digests, pos, act, afirst, n_active, h, pend, cnt);
     return hipGetLastError();
 }
@@ -2462,13 +2487,13 @@ hipError_t launch_chains_absorb(const uint8_t* digests, const uint32_t* pos, con
 hipError_t launch_chains_sum(const uint32_t* which, uint32_t k, const uint32_t* h, const uint32_t* pend,
                              const uint64_t* cnt, uint8_t* out, hipStream_t s) {
     if (k == 0) return hipSuccess;
-    chains_sum_kernel<<<(k + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s>>>(which, k, h, pend, cnt, out);
+    launch_k(chains_sum_kernel, (k + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s, which, k, h, pend, cnt, out);
     return hipGetLastError();
 }
 
 hipError_t launch_chains_reset(const uint32_t* which, uint32_t k, uint32_t* h, uint64_t* cnt, hipStream_t s) {
     if (k == 0) return hipSuccess;
-    chains_reset_kernel<<<(k + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s>>>(which, k, h, cnt);
+    launch_k(chains_reset_kernel, (k + kBlockThreads - 1u) / kBlockThreads, kBlockThreads, 0, s, which, k, h, cnt);
     return hipGetLastError();
 }
 
@@ -2476,7 +2501,7 @@ hipError_t launch_gen_mixed(uint64_t seed, uint64_t first, uint64_t count, const
                             hipStream_t s) {
     if (count == 0) return hipSuccess;
     const uint64_t blocks = std::min<uint64_t>((count + 3u) / 4u, 65536u);
-    gen_mixed_kernel<<<(unsigned)blocks, 256, 0, s>>>(seed, first, count, off, arena);
+    launch_k(gen_mixed_kernel, (unsigned)blocks, 256, 0, s, seed, first, count, off, arena);
     return hipGetLastError();
 }
 
@@ -2485,7 +2510,7 @@ hipError_t launch_gen_requests(uint64_t seed, uint64_t first, uint64_t count, ui
     if (count == 0) return hipSuccess;
     const uint64_t words = count * ((data_len + 7u) / 8u + 2u);
     const uint64_t grid = (words + 255u) / 256u;
-    gen_requests_kernel<<<(unsigned)grid, 256, 0, s>>>(seed, first, count, data_len, arena);
+    launch_k(gen_requests_kernel, (unsigned)grid, 256, 0, s, seed, first, count, data_len, arena);
     return hipGetLastError();
 }
 
