@@ -91,6 +91,14 @@ hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32
 // uniform = B > 0: the lists are identity lists of B entries (list k =
 // entries [k B, min(k B + B, n_entries)), cidx[e] == e); cidx / cfirst unread.
 constexpr uint32_t kOpenEnd = 0xFFFFFFFEu;
+// K[j] + W[j] of a padding-only final block (0x80, zeros, the 64-bit bit
+// length of a message of L bytes, L a multiple of 64): its whole message
+// schedule is a constant (pad_block_kw, host side).
+struct PadBlockKW {
+    uint32_t kw[64];
+    uint32_t use;  // 0: no constant-block path (odd B, or the A/B knob MIRSHA_CHAIN_PAD=0)
+};
+PadBlockKW pad_block_kw(uint64_t L);
 hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                         const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
                         uint8_t* out, hipStream_t s, uint32_t uniform = 0);

@@ -1392,11 +1392,15 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_lists_kernel(
 // requests of a plan (mirsha_plan.hip detects them) -- so bounds and indices
 // are computed, not loaded: the chain's first digest loads issue at once
 // instead of after two dependent loads (cfirst, then cidx).
+// With B even every full list's final block is padding only (32 B digests,
+// 64 B blocks): a wave whose lists all hold B entries runs that block as 64
+// rounds over the precomputed K[j] + W[j] of `pad` (rounds_kw8_asm, ~900
+// instead of ~1,450 instructions on the chain's critical path).
 template <bool kUni>
 __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
     const uint8_t* __restrict__ digests, uint32_t n_digests, const uint32_t* __restrict__ cidx,
     uint32_t n_entries, const uint32_t* __restrict__ cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe,
-    uint32_t* __restrict__ state, uint8_t* __restrict__ out, uint32_t uni) {
+    uint32_t* __restrict__ state, uint8_t* __restrict__ out, uint32_t uni, PadBlockKW pad) {
     __builtin_amdgcn_s_setprio(3);
     const __amdgpu_buffer_rsrc_t drs =
         __builtin_amdgcn_make_buffer_rsrc((void*)digests, (short)0, (int)(32u * n_digests), 0x00020000);
@@ -1425,6 +1429,8 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
     const uint32_t nblk = active ? (full_end - ob) / 2u + (fin ? 1u : 0u) : 0u;
     const uint32_t wave_nb = wave_max(nblk);
     const uint32_t L = 32u * c;
+    // wave-uniform: every lane finishes a full list of B (even) entries here
+    const bool pad_wave = kUni && pad.use && __all(fin && c == uni);
 
     uint32_t st[8];
     if (ob == 0u || !active) {
@@ -1453,7 +1459,17 @@ __global__ __launch_bounds__(kBlockThreads) void sha256_chain_kernel(
         load_digest(drs, nx1, live(t + 1, 1), nxt[2], nxt[3]);
         const uint32_t nn0 = index(ob + 2u * t + 4u, live(t + 2, 0));
         const uint32_t nn1 = index(ob + 2u * t + 5u, live(t + 2, 1));
-        if (t < nblk) {
+        if (pad_wave && t + 1u == wave_nb) {  // the padding-only final block
+            uint32_t s[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) s[i] = st[i];
+#pragma unroll
+            for (int g = 0; g < 8; g++)
+                rounds_kw8_asm(s, make_uint4(pad.kw[8 * g], pad.kw[8 * g + 1], pad.kw[8 * g + 2], pad.kw[8 * g + 3]),
+                               make_uint4(pad.kw[8 * g + 4], pad.kw[8 * g + 5], pad.kw[8 * g + 6], pad.kw[8 * g + 7]));
+#pragma unroll
+            for (int i = 0; i < 8; i++) st[i] += s[i];
+        } else if (t < nblk) {
             uint32_t w[16];
 #pragma unroll
             for (int half = 0; half < 2; half++) {
@@ -2314,6 +2330,22 @@ hipError_t launch_lists(const uint8_t* digests, uint32_t n_digests, const uint32
     return hipGetLastError();
 }
 
+PadBlockKW pad_block_kw(uint64_t L) {
+    auto rotr = [](uint32_t x, int n) { return (x >> n) | (x << (32 - n)); };
+    uint32_t w[64] = {0x80000000u};
+    w[14] = (uint32_t)(L >> 29);  // FIPS 180-4 §5.1.1: the 64-bit bit length, big-endian
+    w[15] = (uint32_t)(L << 3);
+    for (int j = 16; j < 64; j++) {
+        const uint32_t s0 = rotr(w[j - 15], 7) ^ rotr(w[j - 15], 18) ^ (w[j - 15] >> 3);
+        const uint32_t s1 = rotr(w[j - 2], 17) ^ rotr(w[j - 2], 19) ^ (w[j - 2] >> 10);
+        w[j] = w[j - 16] + s0 + w[j - 7] + s1;
+    }
+    PadBlockKW p{};
+    for (int j = 0; j < 64; j++) p.kw[j] = kK[j] + w[j];
+    p.use = 1u;
+    return p;
+}
+
 hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32_t* cidx, uint32_t n_entries,
                         const uint32_t* cfirst, uint32_t n_lists, uint32_t ob, uint32_t oe, uint32_t* state,
                         uint8_t* out, hipStream_t s, uint32_t uniform) {
@@ -2323,11 +2355,17 @@ hipError_t launch_chain(const uint8_t* digests, uint32_t n_digests, const uint32
         // identity lists: list k = entries [k B, ...) must lie inside n_entries
         if ((uint64_t)(n_lists - 1u) * uniform >= n_entries || (uint64_t)n_lists * uniform < n_entries)
             return hipErrorInvalidValue;
-        launch_k(sha256_chain_kernel<true>, grid, kBlockThreads, 0, s, digests, n_digests, cidx, n_entries, cfirst, n_lists,
-                                                                 ob, oe, state, out, uniform);
+        PadBlockKW pad{};
+        if ((uniform & 1u) == 0u) {
+            pad = pad_block_kw(32ull * uniform);
+            const char* e = ab_getenv("MIRSHA_CHAIN_PAD");  // A/B: the generic final block
+            pad.use = !(e && e[0] == '0');
+        }
+        launch_k(sha256_chain_kernel<true>, grid, kBlockThreads, 0, s, digests, n_digests, cidx, n_entries, cfirst,
+                 n_lists, ob, oe, state, out, uniform, pad);
     } else {
         launch_k(sha256_chain_kernel<false>, grid, kBlockThreads, 0, s, digests, n_digests, cidx, n_entries, cfirst,
-                                                                  n_lists, ob, oe, state, out, 0u);
+                 n_lists, ob, oe, state, out, 0u, PadBlockKW{});
     }
     return hipGetLastError();
 }

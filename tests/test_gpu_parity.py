@@ -604,7 +604,9 @@ def _lists(kind, n, bs, rng):
 
 @pytest.mark.parametrize("kind", ["identity", "permuted", "short_middle", "offset"])
 # more than kPairMaxGroups x 64 = 32,768 lists: the chain kernel (fewer go to the pair kernel)
-@pytest.mark.parametrize("n,bs", [(40_000, 1), (70_001, 2), (245_763, 7), (700_003, 20)])
+# even BatchSize: full lists end with a padding-only block (constant-schedule rounds)
+@pytest.mark.parametrize("n,bs", [(40_000, 1), (70_001, 2), (80_000, 2), (245_763, 7), (700_003, 20),
+                                  (655_380, 20)])
 def test_pipeline_uniform_lists(engine, kind, n, bs):
     """Sequential plans over BatchSize lists: identity lists of one size run the
     chain kernel's computed-index form (round 6: no cfirst / cidx loads), every
