@@ -611,10 +611,10 @@ class BatchWorkload:
         e.set_timing_mask([timer])
         e.set_timing(True)
         e.reset_timing()
-        every = max(1, self.a.event_every)
+        every = max(1, min(self.a.event_every, steps))
         t0 = time.perf_counter()
         for i in range(steps):
-            e.set_timing(i % every == 0)  # events ride on every k-th launch (see --event-every)
+            e.set_timing(i % every == every - 1)  # every k-th launch, never the first (see --event-every)
             launch()
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
@@ -1234,7 +1234,9 @@ def main():
         t0 = time.perf_counter()
         for i in range(a.steps):
             if with_events and every > 1:
-                eng.set_timing(i % every == 0)  # events on every k-th step's launch only
+                # every k-th step's launch, never the first after the idle sync: its
+                # dispatch from an idle queue starts late (profiles/r06k)
+                eng.set_timing(i % every == every - 1)
             wl.step()
         torch.cuda.synchronize(dev)
         if dist:
@@ -1245,9 +1247,9 @@ def main():
 
     if a.timed_kernels == "dominant":
         eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED, KERNEL_OVERLAP])
-    every = max(1, a.event_every) if a.events_in_timed_loop else 1
+    every = max(1, min(a.event_every, a.steps)) if a.events_in_timed_loop else 1
     dt = timed(bool(a.events_in_timed_loop), every)
-    ev_steps = len(range(0, a.steps, every))  # steps whose dominant launches carry events
+    ev_steps = len(range(every - 1, a.steps, every))  # steps whose dominant launches carry events
     if not a.events_in_timed_loop:
         timed(True)
     wl.after()
