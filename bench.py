@@ -587,8 +587,8 @@ class BatchWorkload:
         ONE launch per cycle hashes the cycle's requests and the previous
         cycle's batches, as a stream of Ready() cycles pipelines (the state
         machine batches digests of earlier cycles).  Measured after the
-        headline steps on rank 0: --steps launches, the kernel's HIP events
-        on every k-th one (--event-every), wall time and kernel time from that
+        headline steps on rank 0: --steps launches with the kernel's HIP
+        events on (bound to each dispatch), wall time and kernel time from that
         ONE pass (kernel <= wall holds by construction)."""
         if self.plan is None or self.overlap:
             return None
@@ -611,10 +611,13 @@ class BatchWorkload:
         e.set_timing_mask([timer])
         e.set_timing(True)
         e.reset_timing()
-        every = max(1, min(self.a.event_every, steps))
+        # Events on EVERY launch here (bound to the dispatches): the kernel
+        # average is then over the same launches as the wall time, so kernel
+        # <= wall holds (a sampled average need not, profiles/r06l); the
+        # events' dispatch cost (~5 us per launch, profiles/r06h) stays in this
+        # leg's wall time.
         t0 = time.perf_counter()
-        for i in range(steps):
-            e.set_timing(i % every == every - 1)  # every k-th launch, never the first (see --event-every)
+        for _ in range(steps):
             launch()
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
@@ -631,7 +634,7 @@ class BatchWorkload:
                 "note": "one launch per cycle: this cycle's requests + the previous cycle's batch chains "
                         "(mirsha_pipeline_overlap_device, on this plan), steady state of a cycle stream; "
                         "frac = both over the kernel's event time, step_frac = both over ms_per_step; "
-                        "one pass: wall time and the events of every k-th launch (--event-every)"}
+                        "one pass: wall time and the events of every launch (dispatch-bound)"}
 
     def extra(self):
         mode = self.plan.mode_name if self.plan is not None else "none"
