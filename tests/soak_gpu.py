@@ -26,6 +26,7 @@ sys.path.insert(0, HERE)
 import oracle_py  # noqa: E402
 from mirbft_amd import Engine  # noqa: E402
 from mirbft_amd import _lib  # noqa: E402
+from mirbft_amd import sharding  # noqa: E402
 
 EDGE = [0, 1, 15, 16, 17, 55, 56, 63, 64, 65, 119, 120, 127, 128, 183, 184, 247, 248, 272, 4112]
 
@@ -182,7 +183,17 @@ def case_large(eng, rng, seed):
                           d_out.data_ptr())
     eng.sync()
     check(np.array_equal(d_out.cpu().numpy(), want), f"large hash_batch_device n={n} kind={kind}", seed)
-    idx, first = lists_for(rng, n, int(rng.integers(1, 3000)))
+    if rng.integers(0, 2):
+        # BatchSize lists over consecutive requests (sequence.go:154-157), more
+        # than 32,768 of them: the sequential plan's chain kernel, identity lists
+        # in its computed-index form (constant padding block for even sizes),
+        # a permuted near miss in the loaded form
+        bs = int(rng.integers(1, n // 32_769 + 1))
+        idx, first = sharding.batch_lists(n, bs)
+        if rng.integers(0, 4) == 0:
+            idx = rng.permutation(n).astype(np.uint32)
+    else:
+        idx, first = lists_for(rng, n, int(rng.integers(1, 3000)))
     plan = eng.pipeline(n, idx, first, ln, mode=str(rng.choice(["auto", "fused", "sequential"])))
     d_lst = torch.zeros((first.size - 1, 32), dtype=torch.uint8, device="cuda")
     d_out.zero_()
