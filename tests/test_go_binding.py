@@ -2,8 +2,10 @@
 the CPU (verdict r5 item 4; there is no Go toolchain to compile it):
 
 1. every C.mirsha_* call names a function include/mirsha.h declares, with the
-   declared number of arguments, and every C.MIRSHA_* / C.mirsha_* type it
-   names is defined there;
+   declared number of arguments, each argument a pointer or a scalar as the
+   parameter is, of the declared C type where the Go side states it (a cast
+   or a declared variable), and every C.MIRSHA_* / C.mirsha_* type it names
+   is defined there;
 2. every mirsha_* call the Go file makes is made by the C mirrors that run on
    the GPU (tests/c/cgo_sequence.c, tests/c/cgo_path.c);
 3. the mirrored paths make the same calls in the same order: the chunked
@@ -11,8 +13,8 @@ the CPU (verdict r5 item 4; there is no Go toolchain to compile it):
    hash_batch_chunked), gpuHash.Sum vs gpu_sum, and the SubmitBatch / Wait
    and lifecycle sequences inside cgo_sequence.c's main.
 
-The checker is exercised on injected faults: a wrong arity, an unknown
-function, a swapped call order must each fail it."""
+The checker is exercised on injected faults: a wrong arity, a wrong argument
+type or kind, an unknown function, a swapped call order must each fail it."""
 import os
 import re
 
@@ -139,6 +141,83 @@ def check_against_header(go_text, header_text):
     for name in names:
         if name not in macros and name not in types:
             bad.append(f"C.{name}: no such macro or type in mirsha.h")
+    return bad
+
+
+# ---- argument kinds -----------------------------------------------------------
+
+def header_params(text):
+    """{function: [(is_pointer, base type)]} of every mirsha_* declaration."""
+    src = strip_comments(text)
+    out = {}
+    for m in re.finditer(r"\b(mirsha_\w+)\s*\(", src):
+        pre = src[max(0, m.start() - 64):m.start()]
+        if not re.search(r"(int|void|char|mirsha_ctx)\s*\**\s*$", pre):
+            continue
+        params = []
+        for a in split_args(call_args(src, m.end() - 1)):
+            if a == "void":
+                continue
+            words = [w for w in re.findall(r"[A-Za-z_]\w*", a) if w != "const"]
+            params.append(("*" in a, words[0] if words else None))
+        out[m.group(1)] = params
+    return out
+
+
+def go_symbols(src):
+    """{name: (is_pointer, C type or None)} from Go declarations: variables,
+    parameters and struct fields of C.* / *C.* / unsafe.Pointer type."""
+    sym = {}
+    for m in re.finditer(r"\b(\w+)\s+(\*?)C\.(\w+)\b", src):
+        sym[m.group(1)] = (bool(m.group(2)), m.group(3))
+    for m in re.finditer(r"\b(\w+)\s+\*?unsafe\.Pointer\b", src):
+        sym[m.group(1)] = (True, None)
+    for m in re.finditer(r"\b(\w+)\s*:=\s*C\.(\w+)\(", src):
+        sym[m.group(1)] = (False, m.group(2))
+    for m in re.finditer(r"\b(\w+)\s*:=\s*\(\*C\.(\w+)\)\(", src):
+        sym[m.group(1)] = (True, m.group(2))
+    return sym
+
+
+def arg_kind(expr, sym):
+    """(is_pointer, C type or None) of a Go argument expression, or None."""
+    e = expr.strip()
+    m = re.fullmatch(r"C\.(\w+)\(.*\)", e, re.S)
+    if m:
+        return (False, m.group(1))
+    m = re.fullmatch(r"\(\*C\.(\w+)\)\(.*\)", e, re.S)
+    if m:
+        return (True, m.group(1))
+    if e.startswith("&"):
+        return (True, None)
+    if re.fullmatch(r"\d+", e):
+        return (False, None)
+    m = re.fullmatch(r"\*?(?:\w+\.)*(\w+)", e)
+    if m and m.group(1) in sym:
+        return sym[m.group(1)]
+    return None
+
+
+def check_arg_kinds(go_text, header_text):
+    """Problems: a scalar where mirsha.h takes a pointer or the reverse, or a
+    C scalar / pointee type that differs from the declared one."""
+    params = header_params(header_text)
+    src = strip_comments(go_text, go=True)
+    sym = go_symbols(src)
+    bad = []
+    for m in re.finditer(r"\bC\.(mirsha_\w+)\s*\(", src):
+        name = m.group(1)
+        if name not in params:
+            continue
+        for i, (a, (ptr, base)) in enumerate(zip(split_args(call_args(src, m.end() - 1)), params[name])):
+            k = arg_kind(a, sym)
+            if k is None:
+                continue
+            if k[0] != ptr:
+                bad.append(f"C.{name} argument {i + 1} ({a}): {'pointer' if k[0] else 'scalar'} for a "
+                           f"{'pointer' if ptr else 'scalar'} parameter")
+            elif k[1] and base and k[1] != base and not (ptr and base == "void"):
+                bad.append(f"C.{name} argument {i + 1} ({a}): C.{k[1]} for {base}")
     return bad
 
 
@@ -285,6 +364,37 @@ def test_binding_calls_match_header():
     assert len(calls) >= 25 and {"mirsha_submit_batch", "mirsha_submit_arena_multi", "mirsha_hash_batch"} <= {
         c for c, _ in calls}
     assert check_against_header(_read(GO), _read(HEADER)) == []
+
+
+def test_binding_argument_kinds_match_header():
+    assert check_arg_kinds(_read(GO), _read(HEADER)) == []
+    # the checker sees most arguments (casts, &x, literals, declared names)
+    params = header_params(_read(HEADER))
+    src = strip_comments(_read(GO), go=True)
+    sym = go_symbols(src)
+    seen = total = 0
+    for m in re.finditer(r"\bC\.(mirsha_\w+)\s*\(", src):
+        for a in split_args(call_args(src, m.end() - 1)):
+            total += 1
+            seen += arg_kind(a, sym) is not None
+    assert seen / total > 0.9, (seen, total)
+
+
+@pytest.mark.parametrize("fault,needle", [
+    # a 32-bit length where mirsha_submit_batch takes uint64_t arena_len
+    (lambda s: s.replace("(*C.uint8_t)(arena), C.uint64_t(total),", "(*C.uint8_t)(arena), C.uint32_t(total),", 1),
+     "C.uint32_t for uint64_t"),
+    # the ticket by value where mirsha_poll takes int* done
+    (lambda s: s.replace("C.mirsha_poll(g.ctx, t, &d)", "C.mirsha_poll(g.ctx, t, d)", 1), "scalar for a pointer"),
+    # a pointer where mirsha_wait takes the ticket
+    (lambda s: s.replace("C.mirsha_wait(g.ctx, t)", "C.mirsha_wait(g.ctx, &t)", 1), "pointer for a scalar"),
+    # the wrong pointee type
+    (lambda s: s.replace("(*C.uint64_t)(unsafe.Pointer(&off[0]))", "(*C.uint32_t)(unsafe.Pointer(&off[0]))", 1),
+     "C.uint32_t for uint64_t"),
+])
+def test_argument_check_catches_injected_faults(fault, needle):
+    bad = check_arg_kinds(fault(_read(GO)), _read(HEADER))
+    assert any(needle in b for b in bad), bad
 
 
 def test_c_mirrors_match_header():
