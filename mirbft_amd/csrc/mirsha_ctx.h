@@ -235,11 +235,12 @@ int fail(mirsha_ctx* c, int code, const char* fmt, ...);
 
 hipEvent_t take_event(KernelTimer& t);
 
-// Brackets one launch with events on the launch stream when timing is on.
+// One launch (a launch function that launches at most one kernel), timed
+// when timing is on for `which`: the two events ride on the kernel's own
+// dispatch (mirsha::launch_k, hipExtLaunchKernel), so they carry its start
+// and end timestamps and add no marker packets to the stream.
 template <class F>
-int timed_launch_on(mirsha_ctx* c, int which, hipStream_t st, F&& launch) {
-    // The events ride on the kernel's own dispatch (mirsha::launch_k,
-    // hipExtLaunchKernel): its start and end timestamps, no marker packets.
+int timed_launch(mirsha_ctx* c, int which, F&& launch) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->timing && ((c->time_mask >> which) & 1u);
     if (timed) {
@@ -247,7 +248,6 @@ int timed_launch_on(mirsha_ctx* c, int which, hipStream_t st, F&& launch) {
         e1 = take_event(c->timers[which]);
         if (e0 && e1) mirsha::next_launch_events() = {e0, e1};
     }
-    (void)st;
     hipError_t e = launch();
     // unconsumed: the launch function launched nothing (an empty call)
     const bool bound = e0 && e1 && !mirsha::next_launch_events().start;
@@ -259,11 +259,6 @@ int timed_launch_on(mirsha_ctx* c, int which, hipStream_t st, F&& launch) {
     if (e != hipSuccess) return fail(c, MIRSHA_EHIP, "kernel launch: %s", hipGetErrorString(e));
     if (bound) c->timers[which].pending.emplace_back(e0, e1);
     return MIRSHA_OK;
-}
-
-template <class F>
-int timed_launch(mirsha_ctx* c, int which, F&& launch) {
-    return timed_launch_on(c, which, c->stream, launch);
 }
 
 int use_device(mirsha_ctx* c);

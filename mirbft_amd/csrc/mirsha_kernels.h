@@ -67,7 +67,7 @@ constexpr uint32_t kMaxBufferMsgs = 1u << 27;
 // tmp == nullptr only sets tmp_bytes (the scratch size for n requests).
 hipError_t launch_offsets_scan(void* tmp, size_t& tmp_bytes, const uint32_t* len, uint64_t* off, uint32_t n,
                                hipStream_t s);
-// Timing events for the next kernel this thread launches (timed_launch_on):
+// Timing events for the next kernel this thread launches (timed_launch):
 // bound to that kernel's own dispatch through hipExtLaunchKernel, so they
 // carry its start and end timestamps and add no marker packets to the stream
 // (separate hipEventRecord markers around each launch cost ~2.7 us of stream
