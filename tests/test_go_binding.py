@@ -448,6 +448,17 @@ def test_order_check_catches_a_missing_mirror_call():
     assert any("GPUHasher.SubmitBatch" in b for b in bad), bad
 
 
+def test_integration_md_go_snippets_match_header():
+    """The Go snippets left in INTEGRATION.md (Processor wiring, overlapped
+    device cycles) call the C-ABI with the declared names and arities too."""
+    doc = _read(os.path.join(ROOT, "INTEGRATION.md"))
+    blocks = re.findall(r"```go\n(.*?)```", doc, re.S)
+    assert blocks
+    code = "\n".join(blocks)
+    assert check_against_header(code, _read(HEADER)) == []
+    assert any(name == "mirsha_pipeline_overlap_device" for name, _ in go_c_refs(code)[0])
+
+
 def test_go_test_file_uses_only_binding_api():
     """go/gpuhash_test.go calls the binding's exported API only (no C.*), with
     crypto/sha256 as the expected values."""
