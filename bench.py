@@ -1380,9 +1380,10 @@ def main():
                 "step_frac": step_tops / VALU_PEAK_TOPS,
                 "step_achieved": step_tops,
                 "step_compressions_per_gpu": float(tot[2].item()) / world,
-                "frac_note": "frac = the dominant kernel's compressions over its own HIP-event time; step_frac = "
-                             "every compression of a step (request + batch digests, BASELINE.md's accounting) "
-                             "over ms_per_step, per GPU",
+                "frac_note": "frac = the dominant kernel's compressions over its own HIP-event time (events bound "
+                             "to the kernel's dispatches, timed_launches of the timed region: every event_every-th "
+                             "step); step_frac = every compression of a step (request + batch digests, "
+                             "BASELINE.md's accounting) over ms_per_step, per GPU",
                 "traffic": traffic,
                 "kernel": kname,
                 "avg_launch_ms": ms_k / max(n_k, 1),
