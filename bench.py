@@ -132,6 +132,9 @@ def parse():
     p.add_argument("--events-in-timed-loop", type=int, default=1,
                    help="1: per-kernel HIP events inside the timed loop (roofline from the same region); "
                         "0: time the loop bare, then measure kernels in a second identical pass")
+    p.add_argument("--repeat-regions", type=int, default=5,
+                   help="after the headline, time the same --steps region this many more times (bare) and report "
+                        "their per-step median beside the value (SURVEY.md §8d: median over repeats)")
     p.add_argument("--event-every", type=int, default=4,
                    help="inside the timed loop the dominant kernel's HIP events ride on every k-th step's launch "
                         "(bound to its dispatch, hipExtLaunchKernel): an event-bound launch adds ~5 us of stream "
@@ -1266,6 +1269,10 @@ def main():
     # overlap_cycles() resets the engine's timers.
     if hasattr(wl, "batch_ms"):
         wl.batch_ms_timed = wl.batch_ms()
+    # SURVEY.md §8d asks for a median over repeats: the same timed region
+    # --repeat-regions more times, bare (no events), each bracketed like the
+    # headline's; reported beside the value, never as it.
+    rep_ms = [timed(False) / a.steps * 1e3 for _ in range(max(0, a.repeat_regions))]
 
     # Configs 2/3 with a sequential plan: the overlapped-cycles figure, right
     # behind the timed region too (the chip still at its load clock).
@@ -1407,6 +1414,9 @@ def main():
             **wl.extra(),
             "events_in_timed_loop": bool(a.events_in_timed_loop),
             "event_every": every,
+            "repeat_regions": ({"ms_per_step": rep_ms, "median_ms_per_step": float(np.median(rep_ms)),
+                                "note": "the same timed region again, bare, max over ranks not taken; the value "
+                                        "is the first region's"} if rep_ms else None),
             "timed_kernels": a.timed_kernels,
             "self_check": check_all,
             "self_check_scope": "every rank: its own range's first and last batch-aligned windows (the final "
