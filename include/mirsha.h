@@ -93,13 +93,16 @@ void* mirsha_ctx_stream(mirsha_ctx* ctx);
  * environment says. */
 int mirsha_ctx_set_variant(mirsha_ctx* ctx, int variant);
 
-/* Per-kernel device-time accounting with HIP events on the launch stream.
+/* Per-kernel device-time accounting with HIP events bound to each timed
+ * launch's own dispatch (hipExtLaunchKernel): the kernel's start and end
+ * timestamps, no marker packets (an event-bound launch still costs a few us
+ * of stream time, so a benchmark times a sample of its launches).
  * kernel: 0 = message kernel, 1 = digest-list (batch) kernel, 2 = generator
  * and clock probe, 3 = batch-chain kernel, 4 = fused request -> batch kernel
  * (one persistent launch per run), 5 = overlapped-cycles kernel
  * (mirsha_pipeline_overlap_device).
  * set_timing_mask: bit k on = kernel k is timed while timing is enabled
- * (default: all); each timed launch adds two event records to its stream. */
+ * (default: all). */
 int mirsha_ctx_set_timing(mirsha_ctx* ctx, int enable);
 int mirsha_ctx_set_timing_mask(mirsha_ctx* ctx, uint32_t mask);
 int mirsha_ctx_kernel_time(mirsha_ctx* ctx, int kernel, uint64_t* launches, double* total_ms);
