@@ -227,6 +227,15 @@ def _time_cpu(fn, seconds, threads_list):
     return res
 
 
+def event_steps(steps, every):
+    """Steps of a timed region whose dominant launch carries HIP events:
+    every `every`-th from the `every`-th on (never step 0, the first launch
+    after the idle sync, whose dispatch starts late: profiles/r06k); `every`
+    is clamped to the region so at least one step is sampled."""
+    every = max(1, min(int(every), int(steps)))
+    return [i for i in range(steps) if i % every == every - 1]
+
+
 def check_windows(n_batches, batch_size, seed, per_window=256):
     """Batch ranges [b0, b1) the self-check samples: the first window, the
     last (it ends with the final batch, which is short when BatchSize does not
@@ -1237,15 +1246,14 @@ def main():
     def timed(with_events, every=1):
         eng.set_timing(with_events)
         eng.reset_timing()
+        sampled = set(event_steps(a.steps, every))
         if dist:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(a.steps):
             if with_events and every > 1:
-                # every k-th step's launch, never the first after the idle sync: its
-                # dispatch from an idle queue starts late (profiles/r06k)
-                eng.set_timing(i % every == every - 1)
+                eng.set_timing(i in sampled)  # event_steps: every k-th, never the first
             wl.step()
         torch.cuda.synchronize(dev)
         if dist:
@@ -1258,7 +1266,7 @@ def main():
         eng.set_timing_mask([KERNEL_MSGS, KERNEL_FUSED, KERNEL_OVERLAP])
     every = max(1, min(a.event_every, a.steps)) if a.events_in_timed_loop else 1
     dt = timed(bool(a.events_in_timed_loop), every)
-    ev_steps = len(range(every - 1, a.steps, every))  # steps whose dominant launches carry events
+    ev_steps = len(event_steps(a.steps, every))  # steps whose dominant launches carry events
     if not a.events_in_timed_loop:
         timed(True)
     wl.after()

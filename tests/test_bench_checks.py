@@ -112,3 +112,11 @@ def test_evp_pool_on_config2_sample():
     off = np.arange(n, dtype=np.uint64) * stride
     ln = np.full(n, stride, np.uint32)
     assert np.array_equal(o.evp_hash_requests(arena, off, ln, threads=8), o.hash_requests(arena, off, ln))
+
+
+@pytest.mark.parametrize("steps,every,want", [(20, 4, [3, 7, 11, 15, 19]), (20, 1, list(range(20))),
+                                              (5, 4, [3]), (3, 4, [2]), (1, 4, [0]), (50, 4, list(range(3, 50, 4)))])
+def test_event_steps_sample_every_kth_never_the_first(steps, every, want):
+    got = bench.event_steps(steps, every)
+    assert got == want
+    assert got and (0 not in got or steps == 1 or every == 1)
